@@ -1,0 +1,130 @@
+"""Shared helpers for the test suite: synthetic inputs and the CPU oracle loader.
+
+The oracle (oracle/curve_oracle.c -> oracle/liboracle.so) is test
+infrastructure: it is loaded here only to check the product, never by the
+product itself.
+"""
+import ctypes
+import json
+import os
+import subprocess
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+GOLDEN = os.path.join(ROOT, "tests", "golden", "curve_vectors.json")
+
+_GAMMA = np.uint64(0x9E3779B97F4A7C15)
+_M1 = np.uint64(0xBF58476D1CE4E5B9)
+_M2 = np.uint64(0x94D049BB133111EB)
+
+
+def splitmix_words(nwords, seed, start=0):
+    """Counter-based SplitMix64: word i = mix(seed + (i+1)*gamma).  Matches or_splitmix64 and cz_fill."""
+    with np.errstate(over="ignore"):
+        idx = np.arange(start, start + nwords, dtype=np.uint64) + np.uint64(1)
+        z = np.uint64(seed) + idx * _GAMMA
+        z = (z ^ (z >> np.uint64(30))) * _M1
+        z = (z ^ (z >> np.uint64(27))) * _M2
+        return z ^ (z >> np.uint64(31))
+
+
+def splitmix_bytes(n, seed):
+    w = splitmix_words((n + 7) // 8, seed)
+    return w.view(np.uint8)[:n].tobytes()
+
+
+def load_golden():
+    with open(GOLDEN) as f:
+        return json.load(f)
+
+
+# ---- oracle ---------------------------------------------------------------
+_ORACLE = None
+
+
+def oracle():
+    """Load (building if needed) the CPU oracle.  Test infrastructure only."""
+    global _ORACLE
+    if _ORACLE is not None:
+        return _ORACLE
+    path = os.path.join(ROOT, "oracle", "liboracle.so")
+    src = os.path.join(ROOT, "oracle", "curve_oracle.c")
+    if not os.path.exists(path) or os.path.getmtime(path) < os.path.getmtime(src):
+        subprocess.check_call(["make", "-s", "-C", os.path.join(ROOT, "oracle")])
+    lib = ctypes.CDLL(path)
+    P = ctypes.c_char_p
+    U64 = ctypes.c_uint64
+    lib.or_salsa20_core.argtypes = [P, P, P]
+    lib.or_hsalsa20.argtypes = [P, P, P]
+    lib.or_salsa20_xor_ic.argtypes = [P, P, U64, P, U64, P]
+    lib.or_poly1305.argtypes = [P, P, U64, P]
+    lib.or_secretbox.argtypes = [P, P, U64, P, P]
+    lib.or_secretbox.restype = ctypes.c_int
+    lib.or_secretbox_open.argtypes = [P, P, U64, P, P]
+    lib.or_secretbox_open.restype = ctypes.c_int
+    lib.or_curve_encode.argtypes = [P, P, U64, ctypes.c_uint8, U64, ctypes.c_int, P]
+    lib.or_curve_encode.restype = U64
+    lib.or_curve_decode.argtypes = [P, ctypes.POINTER(ctypes.c_uint8), ctypes.POINTER(ctypes.c_uint64), P, U64,
+                                    ctypes.c_int, P]
+    lib.or_curve_decode.restype = ctypes.c_int
+    lib.or_splitmix64.argtypes = [U64, U64]
+    lib.or_splitmix64.restype = U64
+    lib.or_fill.argtypes = [P, U64, U64]
+    lib.or_seal_batch.argtypes = [ctypes.c_void_p, U64, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p,
+                                  ctypes.c_int, ctypes.c_int]
+    _ORACLE = lib
+    return lib
+
+
+def or_hsalsa20(in16, key):
+    out = ctypes.create_string_buffer(32)
+    oracle().or_hsalsa20(out, in16, key)
+    return out.raw
+
+
+def or_salsa20_stream(length, nonce8, ic, key):
+    out = ctypes.create_string_buffer(length)
+    oracle().or_salsa20_xor_ic(out, None, length, nonce8, ic, key)
+    return out.raw
+
+
+def or_poly1305(msg, key):
+    out = ctypes.create_string_buffer(16)
+    oracle().or_poly1305(out, msg, len(msg), key)
+    return out.raw
+
+
+def or_box_afternm(m, n24, k):
+    c = ctypes.create_string_buffer(len(m))
+    rc = oracle().or_secretbox(c, m, len(m), n24, k)
+    return rc, c.raw
+
+
+def or_box_open_afternm(c, n24, k):
+    m = ctypes.create_string_buffer(len(c))
+    rc = oracle().or_secretbox_open(m, c, len(c), n24, k)
+    return rc, m.raw
+
+
+def or_curve_encode(payload, flags, counter, from_server, k):
+    body = ctypes.create_string_buffer(33 + len(payload))
+    n = oracle().or_curve_encode(body, payload, len(payload), flags, counter, from_server, k)
+    assert n == 33 + len(payload)
+    return body.raw
+
+
+def or_curve_decode(body, from_server, k):
+    payload = ctypes.create_string_buffer(max(1, len(body) - 33))
+    flags = ctypes.c_uint8()
+    nonce = ctypes.c_uint64()
+    rc = oracle().or_curve_decode(payload, ctypes.byref(flags), ctypes.byref(nonce), body, len(body), from_server, k)
+    if rc != 0:
+        return rc, None, None, None
+    return 0, payload.raw[: len(body) - 33], flags.value, nonce.value
+
+
+# descriptor layout shared with include/curvezmq_mi355x.h (cz_frame_desc, 40 bytes)
+DESC_DTYPE = np.dtype([("in_off", "<u8"), ("out_off", "<u8"), ("len", "<u4"), ("key_idx", "<u4"),
+                       ("counter", "<u8"), ("flags", "<u4"), ("prev", "<i4")])
+assert DESC_DTYPE.itemsize == 40

@@ -1,0 +1,87 @@
+"""Pin the CPU oracle (oracle/curve_oracle.c) to the golden vectors.
+
+The fixtures come from libsodium 1.0.18 (tests/golden/make_golden.py) because
+the reference's NaCl (jnacl, eu.neilalexander:jnacl:1.0.0, jeromq-core/pom.xml:18-22)
+is not vendored and no JDK exists in this image.  The reference's own tests hold
+no crypto known-answer vectors; the RFC test keys they use
+(org/zeromq/ZMQ.java:4603-4624) drive the MESSAGE vectors here.
+"""
+import pytest
+
+from cz_testlib import (load_golden, or_box_afternm, or_box_open_afternm, or_curve_decode, or_curve_encode,
+                        or_hsalsa20, or_poly1305, or_salsa20_stream, splitmix_bytes)
+
+G = load_golden()
+K = bytes.fromhex(G["keys"]["precom"])
+
+
+def test_subkeys_hoist():
+    # the per-direction HSalsa20 subkey is constant per connection
+    assert or_hsalsa20(b"CurveZMQMESSAGEC", K).hex() == G["keys"]["subkey_c2s"]
+    assert or_hsalsa20(b"CurveZMQMESSAGES", K).hex() == G["keys"]["subkey_s2c"]
+
+
+@pytest.mark.parametrize("v", G["hsalsa20"])
+def test_hsalsa20(v):
+    assert or_hsalsa20(bytes.fromhex(v["in"]), bytes.fromhex(v["key"])).hex() == v["out"]
+
+
+@pytest.mark.parametrize("v", G["salsa20"])
+def test_salsa20_stream(v):
+    s = or_salsa20_stream(v["len"], bytes.fromhex(v["nonce"]), v["ic"], bytes.fromhex(v["key"]))
+    assert s.hex() == v["stream"]
+
+
+@pytest.mark.parametrize("v", G["poly1305"])
+def test_poly1305(v):
+    msg = bytes.fromhex(v["msg_hex"]) if "msg_hex" in v else splitmix_bytes(v["len"], v["msg_seed"])
+    assert or_poly1305(msg, bytes.fromhex(v["key"])).hex() == v["tag"]
+
+
+@pytest.mark.parametrize("v", G["box_afternm"])
+def test_box_afternm_roundtrip(v):
+    key, n24 = bytes.fromhex(v["key"]), bytes.fromhex(v["nonce"])
+    m = bytes(32) + splitmix_bytes(v["n"], v["m_seed"])
+    rc, c = or_box_afternm(m, n24, key)
+    assert rc == 0 and c.hex() == v["c"]
+    rc, m2 = or_box_open_afternm(c, n24, key)
+    assert rc == 0 and m2 == m
+    bad = bytearray(c)
+    bad[-1] ^= 0x80
+    assert or_box_open_afternm(bytes(bad), n24, key)[0] == -1
+
+
+def test_box_short_inputs_rejected():
+    key, n24 = bytes(32), bytes(24)
+    assert or_box_afternm(bytes(31), n24, key)[0] == -1
+    assert or_box_open_afternm(bytes(31), n24, key)[0] == -1
+
+
+@pytest.mark.parametrize("v", G["messages"], ids=lambda v: f"n{v['n']}-s{v['from_server']}-f{v['flags']}-c{v['counter']}")
+def test_curve_message(v):
+    import hashlib
+    payload = splitmix_bytes(v["n"], v["seed"])
+    body = or_curve_encode(payload, v["flags"], v["counter"], v["from_server"], K)
+    assert hashlib.sha256(body).hexdigest() == v["sha256"]
+    assert body[16:32].hex() == v["tag"]
+    if "body" in v:
+        assert body.hex() == v["body"]
+    rc, p2, flags, nonce = or_curve_decode(body, v["from_server"], K)
+    assert rc == 0 and p2 == payload and flags == v["flags"] and nonce == v["counter"]
+    # wrong direction prefix -> cryptographic failure
+    assert or_curve_decode(body, 1 - v["from_server"], K)[0] == -1
+
+
+def test_survey_kat():
+    kat = G["survey_kat"]
+    body = or_curve_encode(bytes.fromhex(kat["payload_hex"]), 0, 3, 0, K)
+    assert body.hex() == kat["body"]
+    assert body[16:32].hex() == "860e3835aa998b0a5b3a9829a03a1189"
+    assert body[32:40].hex() == "a479188bab220f90"
+
+
+def test_decode_rejects_malformed():
+    body = or_curve_encode(b"hello", 0, 3, 0, K)
+    assert or_curve_decode(body[:32], 0, K)[0] == -1
+    bad = b"\x07MESSAGF" + body[8:]
+    assert or_curve_decode(bad, 0, K)[0] == -1

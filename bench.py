@@ -1,0 +1,308 @@
+#!/usr/bin/env python3
+"""CURVE encrypt+MAC throughput on MI355X (BASELINE.json metric).
+
+Workload (BASELINE.json configs[1]): 2^20 x 4 KiB CurveZMQ MESSAGE frames,
+device-resident, sealed per step by one launch of the gfx950 seal kernel
+(Mechanism.encode for every frame: XSalsa20 XOR + Poly1305 tag + MESSAGE
+framing, CurveClientMechanism.java:126-163).  One connection direction (C->S,
+the RFC test keys of org/zeromq/ZMQ.java:4603-4624), counters 3.., every 8th
+frame MORE.  Payload bytes: counter-based SplitMix64, generated on device.
+
+  python bench.py [--gpus N] [--steps K] [--warmup W] [--config 4k|100b|zipf|open4k]
+
+N > 1 (torch.distributed.run, one rank per GPU): every rank seals its own 2^20
+frames (counters offset by rank * 2^20): no collective on the timed path ("weak").
+Rank 0 prints ONE JSON line.  `value` = payload GiB/s over all ranks.
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+import numpy as np
+import torch
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+from jeromq_amd import _lib, batch  # noqa: E402
+
+HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md: 8.0 TB/s)
+PRECOM = bytes.fromhex("0e8790cb0dc8703af2533cc8594eecfbf62ca560a66ebee1259cc0a30435c6f3")  # beforenm(RFC keys)
+FRAMES = 1 << 20
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--config", default="4k", choices=["4k", "100b", "zipf", "open4k"])
+    ap.add_argument("--frames", type=int, default=FRAMES)
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--cpu-seconds", type=float, default=10.0, help="target CPU-baseline sample duration")
+    return ap.parse_args()
+
+
+def setup_dist(args):
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world > 1:
+        import torch.distributed as dist
+        torch.cuda.set_device(local)
+        dist.init_process_group("nccl", device_id=torch.device(f"cuda:{local}"))
+    else:
+        torch.cuda.set_device(0)
+    return world, rank, local
+
+
+def barrier(world):
+    if world > 1:
+        import torch.distributed as dist
+        dist.barrier()
+
+
+def max_over_ranks(world, x):
+    if world == 1:
+        return x
+    import torch.distributed as dist
+    t = torch.tensor([x], dtype=torch.float64, device="cuda")
+    dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    return float(t.item())
+
+
+def sum_over_ranks(world, x):
+    if world == 1:
+        return x
+    import torch.distributed as dist
+    t = torch.tensor([x], dtype=torch.float64, device="cuda")
+    dist.all_reduce(t, op=dist.ReduceOp.SUM)
+    return float(t.item())
+
+
+class Workload:
+    """Builds one rank's device-resident batch and the per-step launch."""
+
+    def __init__(self, cfg, frames, rank, dev):
+        self.cfg = cfg
+        self.dev = dev
+        key = torch.tensor(list(PRECOM), dtype=torch.uint8, device=dev).view(1, 32)
+        self.subkey = batch.subkeys(key, _lib.CZ_DIR_C2S)[0].contiguous()
+        self.counter0 = 3 + rank * frames
+        self.count = frames
+        seed = 0x5EED0000 + {"4k": 1, "100b": 2, "zipf": 3, "open4k": 4}[cfg] + 1000 * rank
+        if cfg in ("4k", "100b", "open4k"):
+            n = 4096 if cfg != "100b" else 100
+            self.n = n
+            self.in_stride = (n + 15) // 16 * 16
+            self.out_stride = (n + 33 + 15) // 16 * 16
+            self.d_in = torch.empty(frames * self.in_stride, dtype=torch.uint8, device=dev)
+            batch.fill(self.d_in, seed)
+            self.flags = torch.zeros(frames, dtype=torch.uint8, device=dev)
+            self.flags[::8] = 1
+            self.d_out = torch.empty(frames * self.out_stride, dtype=torch.uint8, device=dev)
+            self.payload_bytes = frames * n
+            # algorithmic bytes per launch: read payload + flag byte, write 33+n body
+            self.read_bytes = frames * (n + 1)
+            self.write_bytes = frames * (n + 33)
+            if cfg == "open4k":
+                batch.seal_uniform(self.d_in, self.in_stride, self.d_out, self.out_stride, frames, n, self.subkey,
+                                   self.counter0, flags8=self.flags)
+                self.d_plain = torch.empty_like(self.d_in)
+                self.status = torch.empty(frames, dtype=torch.int16, device=dev)
+                # open reads the body + writes payload + 2-byte status (+8 B prev nonce, L2-resident)
+                self.read_bytes = frames * (n + 33)
+                self.write_bytes = frames * (n + 2)
+        else:  # zipf: lengths 64*j, j ~ Zipf(1.2) on 1..1024, seed 42
+            rng = np.random.default_rng(42 + rank)
+            j = np.empty(0, dtype=np.int64)
+            while len(j) < frames:
+                z = rng.zipf(1.2, size=frames)
+                j = np.concatenate([j, z[z <= 1024]])
+            lens = (64 * j[:frames]).astype(np.uint64)
+            desc = np.zeros(frames, dtype=batch.DESC_DTYPE)
+            in_off = np.zeros(frames, dtype=np.uint64)
+            in_off[1:] = np.cumsum(lens[:-1])
+            out_len = (lens + np.uint64(33) + np.uint64(15)) // np.uint64(16) * np.uint64(16)
+            out_off = np.zeros(frames, dtype=np.uint64)
+            out_off[1:] = np.cumsum(out_len[:-1])
+            desc["in_off"] = in_off
+            desc["out_off"] = out_off
+            desc["len"] = lens
+            desc["counter"] = self.counter0 + np.arange(frames, dtype=np.uint64)
+            desc["flags"] = (np.arange(frames) % 8 == 0).astype(np.uint32)
+            desc["prev"] = -1
+            self.desc_np = desc
+            in_bytes = int(lens.sum())
+            out_bytes = int(out_len.sum())
+            self.d_in = torch.empty(in_bytes, dtype=torch.uint8, device=dev)
+            batch.fill(self.d_in, seed)
+            self.d_out = torch.empty(out_bytes, dtype=torch.uint8, device=dev)
+            self.d_desc = torch.from_numpy(desc.view(np.uint8)).to(dev)
+            order = batch.plan_order(desc)
+            self.d_order = torch.from_numpy(order.view(np.int32)).to(dev)
+            self.payload_bytes = in_bytes
+            self.read_bytes = in_bytes + 40 * frames + 4 * frames
+            self.write_bytes = int((lens + np.uint64(33)).sum())
+            self.n = None
+        torch.cuda.synchronize()
+
+    def step(self):
+        if self.cfg in ("4k", "100b"):
+            batch.seal_uniform(self.d_in, self.in_stride, self.d_out, self.out_stride, self.count, self.n,
+                               self.subkey, self.counter0, flags8=self.flags)
+        elif self.cfg == "open4k":
+            batch.open_uniform(self.d_out, self.out_stride, self.d_plain, self.in_stride, self.count, self.n + 33,
+                               self.subkey, self.counter0 - 1, self.status)
+        else:
+            batch.seal_batch(self.d_desc, self.count, self.d_in, self.d_out, self.subkey.view(1, 32),
+                             order=self.d_order)
+
+    def verify_sample(self):
+        """Bit-exact spot check of a few frames against the CPU oracle (test infrastructure)."""
+        sys.path.insert(0, os.path.join(ROOT, "tests"))
+        from cz_testlib import or_curve_encode
+        torch.cuda.synchronize()
+        if self.cfg in ("4k", "100b"):
+            for i in (0, 7, self.count // 2, self.count - 1):
+                p = self.d_in[i * self.in_stride:i * self.in_stride + self.n].cpu().numpy().tobytes()
+                body = self.d_out[i * self.out_stride:i * self.out_stride + self.n + 33].cpu().numpy().tobytes()
+                fl = 1 if i % 8 == 0 else 0
+                if body != or_curve_encode(p, fl, self.counter0 + i, 0, PRECOM):
+                    raise SystemExit(f"parity failure at frame {i}")
+        elif self.cfg == "open4k":
+            st = self.status.cpu().numpy().view(np.uint16)
+            if np.any(st & 0xff):
+                raise SystemExit("open failures in benchmark batch")
+            if not torch.equal(self.d_plain, self.d_in):
+                raise SystemExit("open round trip mismatch")
+        else:
+            for i in (0, 1, self.count - 1):
+                d = self.desc_np[i]
+                p = self.d_in[int(d["in_off"]):int(d["in_off"]) + int(d["len"])].cpu().numpy().tobytes()
+                body = self.d_out[int(d["out_off"]):int(d["out_off"]) + int(d["len"]) + 33].cpu().numpy().tobytes()
+                if body != or_curve_encode(p, int(d["flags"]), int(d["counter"]), 0, PRECOM):
+                    raise SystemExit(f"parity failure at frame {i}")
+
+
+def cpu_baseline(wl, target_s):
+    """The oracle (oracle/curve_oracle.c, a scalar C restatement of the NaCl path) timed on the
+    host: 1 thread, a bounded sample of the same frames.  Reported, not the target."""
+    sys.path.insert(0, os.path.join(ROOT, "tests"))
+    from cz_testlib import oracle
+    lib = oracle()
+    n = wl.n if wl.n else 4096
+    stride = (n + 15) // 16 * 16
+    ostride = (n + 33 + 15) // 16 * 16
+
+    def run(count):
+        hin = np.frombuffer(np.random.default_rng(1).bytes(count * stride), dtype=np.uint8).copy()
+        hout = np.zeros(count * ostride, dtype=np.uint8)
+        desc = np.zeros(count, dtype=batch.DESC_DTYPE)
+        desc["in_off"] = np.arange(count, dtype=np.uint64) * stride
+        desc["out_off"] = np.arange(count, dtype=np.uint64) * ostride
+        desc["len"] = n
+        desc["counter"] = 3 + np.arange(count, dtype=np.uint64)
+        precom = np.frombuffer(PRECOM, dtype=np.uint8).copy()
+        t0 = time.perf_counter()
+        lib.or_seal_batch(desc.ctypes.data, count, hin.ctypes.data, hout.ctypes.data, precom.ctypes.data, 0, 1)
+        return time.perf_counter() - t0
+
+    probe = 256 if n > 1000 else 8192
+    dt = run(probe)
+    count = int(max(probe, min(probe * target_s / max(dt, 1e-6), 4_000_000)))
+    dt = run(count)
+    gibs = count * n / dt / 2**30
+    return {"value": round(gibs, 4), "unit": "GiB/s", "cores": 1, "kind": "port",
+            "sample": f"{count} x {n} B frames sealed by oracle/curve_oracle.c (1 thread, {dt:.1f} s), "
+                      f"{os.cpu_count()} logical CPUs visible"}
+
+
+def load_pmc_traffic(cfg):
+    """HBM bytes per launch from the committed rocprofv3 PMC summary, if one exists for this config."""
+    path = os.path.join(ROOT, "profiles", "pmc_traffic.json")
+    if not os.path.exists(path):
+        return None
+    try:
+        with open(path) as f:
+            d = json.load(f)
+        v = d.get(cfg)
+        return None if v is None else float(v["hbm_bytes_per_launch"])
+    except Exception:
+        return None
+
+
+def main():
+    args = parse()
+    world, rank, local = setup_dist(args)
+    dev = torch.device(f"cuda:{local}")
+    wl = Workload(args.config, args.frames, rank, dev)
+
+    for _ in range(args.warmup):
+        wl.step()
+    torch.cuda.synchronize()
+    wl.verify_sample()
+
+    stream = torch.cuda.current_stream()
+    evs = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(args.steps)]
+    barrier(world)
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for a, b in evs:
+        a.record(stream)
+        wl.step()
+        b.record(stream)
+    torch.cuda.synchronize()
+    barrier(world)
+    elapsed = time.perf_counter() - t0
+    kern_ms = [a.elapsed_time(b) for a, b in evs]
+    avg_kernel_s = float(np.mean(kern_ms)) / 1e3
+
+    elapsed = max_over_ranks(world, elapsed)
+    total_payload = sum_over_ranks(world, float(wl.payload_bytes) * args.steps)
+    value = total_payload / elapsed / 2**30
+    alg_bytes = wl.read_bytes + wl.write_bytes
+    achieved = alg_bytes / avg_kernel_s / 1e9
+    traffic = load_pmc_traffic(args.config)
+
+    cpu = None
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        cpu = cpu_baseline(wl, args.cpu_seconds)
+
+    if rank == 0:
+        names = {"4k": "1M x 4 KiB frames, seal (configs[1])", "100b": "1M x 100 B frames, seal (configs[2])",
+                 "zipf": "1M Zipf(1.2) 64 B..64 KiB frames, seal (configs[3])",
+                 "open4k": "1M x 4 KiB frames, open+verify (configs[4] leg)"}
+        line = {
+            "metric": "CURVE encrypt+MAC GiB/s (device-resident), batched 4 KiB frames, 1/2/4/8 GPU",
+            "value": round(value, 3),
+            "unit": "GiB/s",
+            "n_gpus": world,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": round(elapsed / args.steps * 1e3, 4),
+            "higher_is_better": True,
+            "scaling": "weak",
+            "vs_baseline": None,
+            "dtype": "u32",
+            "data": "synthetic (SplitMix64 payload on device, RFC test keys)",
+            "config": {"workload": names[args.config], "frames_per_gpu": wl.count,
+                       "payload_bytes_per_gpu": wl.payload_bytes, "parallelism": f"shard{world}",
+                       "frames_per_s": round(wl.count * world * args.steps / elapsed, 1)},
+            "roofline": {"bound": "hbm", "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                         "frac": round(achieved / HBM_PEAK_GBS, 4),
+                         "traffic": traffic,
+                         "kernel_ms": round(avg_kernel_s * 1e3, 4),
+                         "alg_bytes_per_launch": alg_bytes},
+            "cpu_baseline": cpu,
+        }
+        print(json.dumps(line), flush=True)
+    if world > 1:
+        import torch.distributed as dist
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

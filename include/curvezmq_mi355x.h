@@ -1,0 +1,198 @@
+/*
+ * curvezmq_mi355x.h -- C-ABI of the MI355X CurveZMQ MESSAGE crypto path.
+ *
+ * This library replaces, for JeroMQ's CURVE sockets, the per-message NaCl calls
+ * that JeroMQ makes through the third-party jnacl artefact
+ * (eu.neilalexander:jnacl:1.0.0, jeromq-core/pom.xml:18-22; imported at
+ * jeromq-core/src/main/java/zmq/io/mechanism/curve/Curve.java:5-6).
+ * Every entry point is plain C: pointers, sizes, ints.  Device pointers are
+ * HIP device addresses; `stream` is a hipStream_t passed as void* (NULL = the
+ * null stream).  All batched launchers are asynchronous, allocate nothing and
+ * never synchronise, so they may be captured into a hipGraph.
+ *
+ * Return conventions
+ *   jnacl drop-ins (section 1): 0 on success, -1 on failure -- exactly the
+ *   int contract of crypto_box_afternm / crypto_box_open_afternm that
+ *   Curve.java:134-147 forwards to callers (encode asserts rc == 0,
+ *   CurveClientMechanism.java:153-154; decode maps -1 to EPROTO,
+ *   CurveClientMechanism.java:218-223).
+ *   Everything else: CZ_OK (0) or a negative CZ_E* code; cz_last_error()
+ *   returns a thread-local message.
+ *
+ * Thread safety: all functions are reentrant.  The single-shot calls use a
+ * per-thread device context (JeroMQ runs one connection per IO thread,
+ * StreamEngine.java:467-535); cz_ctx objects must not be shared between
+ * threads without external locking.
+ */
+#ifndef CURVEZMQ_MI355X_H
+#define CURVEZMQ_MI355X_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+/* Sizes: Curve.Size (Curve.java:14-67) / jnacl crypto_secretbox_* constants */
+#define CZ_NONCEBYTES 24
+#define CZ_ZEROBYTES 32
+#define CZ_BOXZEROBYTES 16
+#define CZ_KEYBYTES 32
+#define CZ_BEFORENMBYTES 32
+#define CZ_MACBYTES 16
+/* MESSAGE body = "\x07MESSAGE"(8) + nonce8 + tag16 + flags(1) + payload */
+#define CZ_MESSAGE_OVERHEAD 33
+
+/* Msg flags carried in the encrypted flags byte (Msg.java:96-100, CurveClientMechanism.java:131-137) */
+#define CZ_MSG_MORE 0x01
+#define CZ_MSG_COMMAND 0x02
+
+/* direction of a connection-direction subkey (nonce prefix, CurveClientMechanism.java:141, :182) */
+#define CZ_DIR_C2S 0 /* "CurveZMQMESSAGEC": sealed by the client, opened by the server */
+#define CZ_DIR_S2C 1 /* "CurveZMQMESSAGES": sealed by the server, opened by the client */
+
+/* Per-frame status of an open (low byte) -- what Mechanism.decode would have raised */
+#define CZ_STATUS_OK 0
+#define CZ_STATUS_CRYPTO 1    /* bad tag: ZMQ_PROTOCOL_ERROR_ZMTP_CRYPTOGRAPHIC (zmq/ZMQ.java:227) */
+#define CZ_STATUS_MALFORMED 2 /* size < 33: ZMTP_MALFORMED_COMMAND_MESSAGE (CurveClientMechanism.java:174-178) */
+#define CZ_STATUS_COMMAND 3   /* not "\x07MESSAGE": ZMTP_UNEXPECTED_COMMAND (CurveClientMechanism.java:168-172) */
+#define CZ_STATUS_SEQUENCE 4  /* nonce <= previous: replay (CurveClientMechanism.java:186-193) */
+/* bits 8..15 of an OK status hold the decrypted flags byte (CZ_MSG_MORE / CZ_MSG_COMMAND) */
+
+/* Library error codes */
+#define CZ_OK 0
+#define CZ_EINVAL (-22)
+#define CZ_EHIP (-5)
+#define CZ_ENOMEM (-12)
+#define CZ_EPROTO (-71)
+
+/* cz_frame_desc.flags bits (seal: low byte = the MESSAGE flags byte) */
+#define CZ_DESC_CHECK_NONCE 0x100 /* open: enforce nonce > floor (counter or prev frame's nonce) */
+
+/*
+ * One frame of a batch (40 bytes).  Offsets are byte offsets into the batch's
+ * in / out buffers; 16-byte aligned offsets take the vectorised fast path.
+ *   seal: in  = payload (len = n bytes)      out = MESSAGE body (n + 33 bytes)
+ *         counter = the 8-byte nonce counter (cnNonce), flags low byte = MORE|COMMAND
+ *   open: in  = MESSAGE body (len = size)    out = payload (size - 33 bytes)
+ *         counter = replay floor (cnPeerNonce) used when prev < 0;
+ *         prev >= 0: the floor is the nonce of frame `prev` of this batch (same connection)
+ *   key_idx selects the 32-byte Salsa20 subkey in the batch's subkey table.
+ */
+typedef struct cz_frame_desc {
+    uint64_t in_off;
+    uint64_t out_off;
+    uint32_t len;
+    uint32_t key_idx;
+    uint64_t counter;
+    uint32_t flags;
+    int32_t prev;
+} cz_frame_desc;
+
+/* ---- 1. jnacl drop-ins (host memory, NaCl ZEROBYTES layouts) -------------------
+ * Replaces curve25519xsalsa20poly1305.crypto_box_afternm (called at Curve.java:136)
+ * and crypto_box_open_afternm (Curve.java:146); crypto_secretbox[_open]
+ * (xsalsa20poly1305, Curve.java:166,176) is the same primitive.
+ * m[0:32] must be zero; c[0:16] is written as zero.  Runs on the GPU (one
+ * launch per call: latency-bound -- use the batched API for throughput). */
+int cz_box_afternm(uint8_t *c, const uint8_t *m, uint64_t mlen, const uint8_t n[24], const uint8_t k[32]);
+int cz_box_open_afternm(uint8_t *m, const uint8_t *c, uint64_t clen, const uint8_t n[24], const uint8_t k[32]);
+int cz_secretbox(uint8_t *c, const uint8_t *m, uint64_t mlen, const uint8_t n[24], const uint8_t k[32]);
+int cz_secretbox_open(uint8_t *m, const uint8_t *c, uint64_t clen, const uint8_t n[24], const uint8_t k[32]);
+
+/* ---- 2. key schedule ------------------------------------------------------------
+ * Per-connection-direction Salsa20 subkey = HSalsa20(cnPrecom, "CurveZMQMESSAGE{C|S}").
+ * The MESSAGE nonce is that constant 16-byte prefix + BE64(counter)
+ * (CurveClientMechanism.java:139-142), so XSalsa20's HSalsa20 step is hoisted
+ * out of the per-message path.  d_precom / d_subkeys: nkeys x 32 bytes (device). */
+int cz_subkeys(void *d_subkeys, const void *d_precom, uint32_t nkeys, int direction, void *stream);
+/* host convenience: one subkey (runs the same device kernel, synchronously) */
+int cz_subkey(uint8_t out[32], const uint8_t k[32], int direction);
+
+/* ---- 3. batched, device-resident -----------------------------------------------
+ * Mechanism.encode / decode for `count` independent frames in one launch.
+ * d_order (optional, count x u32) permutes the lane->frame assignment: pass the
+ * frames sorted by decreasing length to balance ragged batches (cz_plan_order). */
+int cz_seal_batch(const cz_frame_desc *d_desc, const uint32_t *d_order, uint32_t count, const void *d_in,
+                  void *d_out, const void *d_subkeys, void *stream);
+/* d_status[i] = CZ_STATUS_* | (flags << 8); d_nonces (optional) = the frame's nonce counter */
+int cz_open_batch(const cz_frame_desc *d_desc, const uint32_t *d_order, uint32_t count, const void *d_in,
+                  void *d_out, const void *d_subkeys, uint16_t *d_status, uint64_t *d_nonces, void *stream);
+
+/* Uniform-length batch of ONE connection direction: frame i at in + i*in_stride,
+ * body i at out + i*out_stride, nonce counter0 + i, flags d_flags8[i] (NULL = 0). */
+int cz_seal_uniform(uint32_t count, uint32_t len, const void *d_in, uint64_t in_stride, void *d_out,
+                    uint64_t out_stride, const void *d_subkey, uint64_t counter0, const uint8_t *d_flags8,
+                    void *stream);
+/* Open `count` bodies of `size` bytes of one connection in order; frame 0 must
+ * beat floor0, frame i must beat frame i-1 (when check != 0). */
+int cz_open_uniform(uint32_t count, uint32_t size, const void *d_in, uint64_t in_stride, void *d_out,
+                    uint64_t out_stride, const void *d_subkey, uint64_t floor0, int check, uint16_t *d_status,
+                    void *stream);
+
+/* Host-side planner: order[] = frame indices sorted by decreasing len (stable). */
+int cz_plan_order(const cz_frame_desc *h_desc, uint32_t count, uint32_t *h_order);
+
+/* Synthetic data: fill d_buf with the counter-based SplitMix64 byte stream (seed). */
+int cz_fill(void *d_buf, uint64_t nbytes, uint64_t seed, void *stream);
+
+/* ---- 4. host-staged batches (the JNI path: Java byte[] / direct ByteBuffer) -------
+ * A context owns a HIP stream, pinned host staging and device buffers that grow
+ * on demand.  cz_ctx_seal/open copy host frames in, run the batch kernel and copy
+ * the results out (synchronous).  These are what a JNI shim binds. */
+typedef struct cz_ctx cz_ctx;
+int cz_ctx_create(cz_ctx **out, int device);
+void cz_ctx_destroy(cz_ctx *ctx);
+/* upload `nkeys` 32-byte cnPrecom keys and derive their subkeys for `direction` */
+int cz_ctx_set_keys(cz_ctx *ctx, const uint8_t *h_precom, uint32_t nkeys, int direction);
+int cz_ctx_seal(cz_ctx *ctx, const cz_frame_desc *h_desc, uint32_t count, const void *h_in, uint64_t in_bytes,
+                void *h_out, uint64_t out_bytes);
+int cz_ctx_open(cz_ctx *ctx, const cz_frame_desc *h_desc, uint32_t count, const void *h_in, uint64_t in_bytes,
+                void *h_out, uint64_t out_bytes, uint16_t *h_status);
+/* pinned host buffers for zero-extra-copy callers (a pinned MsgAllocator, zmq/msg/MsgAllocator.java:5-8) */
+void *cz_host_alloc(uint64_t bytes);
+void cz_host_free(void *p);
+
+/* ---- 5. CURVE mechanism objects (host mirror of CurveClientMechanism / CurveServerMechanism
+ *         in the CONNECTED state: encode/decode of MESSAGE commands with nonce bookkeeping) ---- */
+typedef struct cz_mech cz_mech;
+/* as_server = 0: client (seals ...MESSAGEC, opens ...MESSAGES); 1: server.
+ * cn_nonce / cn_peer_nonce: the handshake's final values (client
+ * MESSAGEs start at 3, server at 2). */
+cz_mech *cz_mech_create(int as_server, const uint8_t precom[32], uint64_t cn_nonce, uint64_t cn_peer_nonce,
+                        int device);
+void cz_mech_destroy(cz_mech *m);
+/* encode one Msg: out must hold n + 33 bytes; returns the body length or a negative CZ_E* */
+int64_t cz_mech_encode(cz_mech *m, const uint8_t *payload, uint64_t n, int msg_flags, uint8_t *out);
+/* decode one body: returns the payload length (>= 0) and *msg_flags, or CZ_EPROTO with
+ * *event = ZMQ_PROTOCOL_ERROR_* code (zmq/ZMQ.java:209-227) the reference would raise */
+int64_t cz_mech_decode(cz_mech *m, const uint8_t *body, uint64_t size, uint8_t *out, int *msg_flags, int *event);
+/* batched encode of count frames packed back to back: payloads at in_off[i] (len[i]),
+ * bodies written at out_off[i].  One device launch for the whole batch. */
+int cz_mech_encode_batch(cz_mech *m, uint32_t count, const uint8_t *h_in, const uint64_t *in_off,
+                         const uint32_t *len, const uint8_t *msg_flags, uint8_t *h_out, const uint64_t *out_off);
+/* batched decode: stops at the first failing frame like StreamEngine does (returns its index
+ * in *failed, or -1); frames before it are delivered. */
+int cz_mech_decode_batch(cz_mech *m, uint32_t count, const uint8_t *h_in, const uint64_t *in_off,
+                         const uint32_t *size, uint8_t *h_out, const uint64_t *out_off, uint8_t *msg_flags,
+                         int32_t *failed, int *event);
+uint64_t cz_mech_nonce(const cz_mech *m);
+uint64_t cz_mech_peer_nonce(const cz_mech *m);
+
+/* ZMTP protocol-error event codes (zmq/ZMQ.java:214-227) */
+#define CZ_ZMTP_UNEXPECTED_COMMAND 0x10000001
+#define CZ_ZMTP_MALFORMED_COMMAND_MESSAGE 0x10000012
+#define CZ_ZMTP_INVALID_SEQUENCE 0x10000002
+#define CZ_ZMTP_CRYPTOGRAPHIC 0x11000001
+
+/* ---- 6. misc -------------------------------------------------------------- */
+const char *cz_last_error(void);
+const char *cz_version(void);
+/* 1 if a HIP device is present and the gfx950 code object loaded */
+int cz_device_ok(void);
+
+#ifdef __cplusplus
+}
+#endif
+#endif

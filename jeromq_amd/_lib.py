@@ -1,0 +1,119 @@
+"""ctypes binding of libcurvezmq_mi355x.so (the C-ABI in include/curvezmq_mi355x.h).
+
+The library is the product: every byte of ciphertext, plaintext and every tag
+comes from its gfx950 kernels.  There is no CPU fallback -- if the shared
+object is missing this module raises, and on a machine without a GPU the
+compute entry points return CZ_EHIP.
+"""
+import ctypes
+import os
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(HERE, "libcurvezmq_mi355x.so")
+
+CZ_OK = 0
+CZ_EINVAL = -22
+CZ_EHIP = -5
+CZ_ENOMEM = -12
+CZ_EPROTO = -71
+
+CZ_STATUS_OK = 0
+CZ_STATUS_CRYPTO = 1
+CZ_STATUS_MALFORMED = 2
+CZ_STATUS_COMMAND = 3
+CZ_STATUS_SEQUENCE = 4
+
+CZ_DIR_C2S = 0
+CZ_DIR_S2C = 1
+CZ_MSG_MORE = 0x01
+CZ_MSG_COMMAND = 0x02
+CZ_DESC_CHECK_NONCE = 0x100
+CZ_MESSAGE_OVERHEAD = 33
+
+CZ_ZMTP_UNEXPECTED_COMMAND = 0x10000001
+CZ_ZMTP_MALFORMED_COMMAND_MESSAGE = 0x10000012
+CZ_ZMTP_INVALID_SEQUENCE = 0x10000002
+CZ_ZMTP_CRYPTOGRAPHIC = 0x11000001
+
+
+class CzError(RuntimeError):
+    pass
+
+
+class cz_frame_desc(ctypes.Structure):
+    _fields_ = [("in_off", ctypes.c_uint64), ("out_off", ctypes.c_uint64), ("len", ctypes.c_uint32),
+                ("key_idx", ctypes.c_uint32), ("counter", ctypes.c_uint64), ("flags", ctypes.c_uint32),
+                ("prev", ctypes.c_int32)]
+
+
+assert ctypes.sizeof(cz_frame_desc) == 40
+
+_VP = ctypes.c_void_p
+_P = ctypes.c_char_p
+_U8P = ctypes.POINTER(ctypes.c_uint8)
+_U32 = ctypes.c_uint32
+_U64 = ctypes.c_uint64
+_I = ctypes.c_int
+
+# name -> (restype, argtypes); must cover every function in include/curvezmq_mi355x.h
+SIGNATURES = {
+    "cz_box_afternm": (_I, [_VP, _VP, _U64, _VP, _VP]),
+    "cz_box_open_afternm": (_I, [_VP, _VP, _U64, _VP, _VP]),
+    "cz_secretbox": (_I, [_VP, _VP, _U64, _VP, _VP]),
+    "cz_secretbox_open": (_I, [_VP, _VP, _U64, _VP, _VP]),
+    "cz_subkeys": (_I, [_VP, _VP, _U32, _I, _VP]),
+    "cz_subkey": (_I, [_VP, _VP, _I]),
+    "cz_seal_batch": (_I, [_VP, _VP, _U32, _VP, _VP, _VP, _VP]),
+    "cz_open_batch": (_I, [_VP, _VP, _U32, _VP, _VP, _VP, _VP, _VP, _VP]),
+    "cz_seal_uniform": (_I, [_U32, _U32, _VP, _U64, _VP, _U64, _VP, _U64, _VP, _VP]),
+    "cz_open_uniform": (_I, [_U32, _U32, _VP, _U64, _VP, _U64, _VP, _U64, _I, _VP, _VP]),
+    "cz_plan_order": (_I, [_VP, _U32, _VP]),
+    "cz_fill": (_I, [_VP, _U64, _U64, _VP]),
+    "cz_ctx_create": (_I, [ctypes.POINTER(_VP), _I]),
+    "cz_ctx_destroy": (None, [_VP]),
+    "cz_ctx_set_keys": (_I, [_VP, _VP, _U32, _I]),
+    "cz_ctx_seal": (_I, [_VP, _VP, _U32, _VP, _U64, _VP, _U64]),
+    "cz_ctx_open": (_I, [_VP, _VP, _U32, _VP, _U64, _VP, _U64, _VP]),
+    "cz_host_alloc": (_VP, [_U64]),
+    "cz_host_free": (None, [_VP]),
+    "cz_mech_create": (_VP, [_I, _VP, _U64, _U64, _I]),
+    "cz_mech_destroy": (None, [_VP]),
+    "cz_mech_encode": (ctypes.c_int64, [_VP, _VP, _U64, _I, _VP]),
+    "cz_mech_decode": (ctypes.c_int64, [_VP, _VP, _U64, _VP, ctypes.POINTER(_I), ctypes.POINTER(_I)]),
+    "cz_mech_encode_batch": (_I, [_VP, _U32, _VP, _VP, _VP, _VP, _VP, _VP]),
+    "cz_mech_decode_batch": (_I, [_VP, _U32, _VP, _VP, _VP, _VP, _VP, _VP, _VP, ctypes.POINTER(_I)]),
+    "cz_mech_nonce": (_U64, [_VP]),
+    "cz_mech_peer_nonce": (_U64, [_VP]),
+    "cz_last_error": (ctypes.c_char_p, []),
+    "cz_version": (ctypes.c_char_p, []),
+    "cz_device_ok": (_I, []),
+}
+
+_LIB = None
+
+
+def lib():
+    """Load the HIP library; raise loudly if it has not been built."""
+    global _LIB
+    if _LIB is not None:
+        return _LIB
+    if not os.path.exists(LIB_PATH):
+        raise CzError(f"{LIB_PATH} is missing: run `python -m jeromq_amd.build` (hipcc, gfx950). "
+                      "There is no CPU fallback for the CURVE path.")
+    L = ctypes.CDLL(LIB_PATH)
+    for name, (res, args) in SIGNATURES.items():
+        f = getattr(L, name)
+        f.restype = res
+        f.argtypes = args
+    _LIB = L
+    return L
+
+
+def last_error():
+    return lib().cz_last_error().decode(errors="replace")
+
+
+def check(rc, what="cz call"):
+    if rc != CZ_OK:
+        raise CzError(f"{what} failed ({rc}): {last_error()}")
+    return rc

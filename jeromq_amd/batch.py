@@ -1,0 +1,110 @@
+"""Device-resident batched seal/open over torch tensors (torch = HBM allocator + streams only).
+
+All functions launch asynchronously on `stream` (default: torch's current
+stream) and return immediately; the crypto runs in the gfx950 kernels of
+libcurvezmq_mi355x.so.
+"""
+import numpy as np
+
+from . import _lib
+
+
+def _stream(stream):
+    import torch
+    if stream is None:
+        return torch.cuda.current_stream().cuda_stream
+    return getattr(stream, "cuda_stream", stream)
+
+
+def _ptr(t):
+    return None if t is None else t.data_ptr()
+
+
+def _need_cuda_u8(t, what):
+    import torch
+    if t is None or not t.is_cuda:
+        raise ValueError(f"{what} must be a CUDA (HIP) tensor")
+    if t.dtype != torch.uint8 and what not in ("desc",):
+        raise ValueError(f"{what} must be uint8")
+
+
+def subkeys(precom, direction, stream=None):
+    """precom: (nkeys, 32) uint8 device tensor -> (nkeys, 32) subkeys for `direction`."""
+    import torch
+    _need_cuda_u8(precom, "precom")
+    out = torch.empty_like(precom)
+    _lib.check(_lib.lib().cz_subkeys(_ptr(out), _ptr(precom), precom.shape[0], direction, _stream(stream)),
+               "cz_subkeys")
+    return out
+
+
+def seal_uniform(inp, in_stride, out, out_stride, count, length, subkey, counter0, flags8=None, stream=None):
+    _need_cuda_u8(inp, "in")
+    _need_cuda_u8(out, "out")
+    need_in = (count - 1) * in_stride + length if count else 0
+    need_out = (count - 1) * out_stride + length + _lib.CZ_MESSAGE_OVERHEAD if count else 0
+    if inp.numel() < need_in or out.numel() < need_out:
+        raise ValueError("buffer too small for the batch")
+    if flags8 is not None and flags8.numel() < count:
+        raise ValueError("flags8 too small")
+    _lib.check(_lib.lib().cz_seal_uniform(count, length, _ptr(inp), in_stride, _ptr(out), out_stride, _ptr(subkey),
+                                          counter0, _ptr(flags8), _stream(stream)), "cz_seal_uniform")
+
+
+def open_uniform(inp, in_stride, out, out_stride, count, size, subkey, floor0, status, check=True, stream=None):
+    _need_cuda_u8(inp, "in")
+    _need_cuda_u8(out, "out")
+    if count and (inp.numel() < (count - 1) * in_stride + size or status.numel() < count):
+        raise ValueError("buffer too small for the batch")
+    if count and size >= 33 and out.numel() < (count - 1) * out_stride + size - 33:
+        raise ValueError("output too small for the batch")
+    _lib.check(_lib.lib().cz_open_uniform(count, size, _ptr(inp), in_stride, _ptr(out), out_stride, _ptr(subkey),
+                                          floor0, 1 if check else 0, _ptr(status), _stream(stream)),
+               "cz_open_uniform")
+
+
+def _check_desc_bounds(desc_np, in_bytes, out_bytes, nkeys, seal):
+    ln = desc_np["len"].astype(np.uint64)
+    olen = ln + np.uint64(33) if seal else np.where(ln >= 33, ln - np.uint64(33), 0).astype(np.uint64)
+    if len(desc_np) and (np.any(desc_np["in_off"] + ln > np.uint64(in_bytes))
+                         or np.any(desc_np["out_off"] + olen > np.uint64(out_bytes))
+                         or np.any(desc_np["key_idx"] >= nkeys)):
+        raise ValueError("descriptor out of bounds")
+
+
+def seal_batch(desc, count, inp, out, subkeys_t, order=None, stream=None, desc_np=None):
+    """desc: device tensor holding `count` cz_frame_desc (40 B each).  If desc_np (the host
+    copy, numpy DESC dtype) is given, bounds are checked before the launch."""
+    _need_cuda_u8(inp, "in")
+    _need_cuda_u8(out, "out")
+    if desc_np is not None:
+        _check_desc_bounds(desc_np, inp.numel(), out.numel(), subkeys_t.shape[0], True)
+    _lib.check(_lib.lib().cz_seal_batch(_ptr(desc), _ptr(order), count, _ptr(inp), _ptr(out), _ptr(subkeys_t),
+                                        _stream(stream)), "cz_seal_batch")
+
+
+def open_batch(desc, count, inp, out, subkeys_t, status, nonces=None, order=None, stream=None, desc_np=None):
+    _need_cuda_u8(inp, "in")
+    _need_cuda_u8(out, "out")
+    if desc_np is not None:
+        _check_desc_bounds(desc_np, inp.numel(), out.numel(), subkeys_t.shape[0], False)
+    _lib.check(_lib.lib().cz_open_batch(_ptr(desc), _ptr(order), count, _ptr(inp), _ptr(out), _ptr(subkeys_t),
+                                        _ptr(status), _ptr(nonces), _stream(stream)), "cz_open_batch")
+
+
+def fill(buf, seed, stream=None):
+    """Counter-based SplitMix64 synthetic bytes (tests/cz_testlib.py splitmix_words)."""
+    _lib.check(_lib.lib().cz_fill(_ptr(buf), buf.numel() * buf.element_size(), seed, _stream(stream)), "cz_fill")
+
+
+def plan_order(desc_np):
+    """Frame indices sorted by decreasing length (balances lanes of a ragged batch)."""
+    count = len(desc_np)
+    order = np.zeros(count, dtype=np.uint32)
+    d = np.ascontiguousarray(desc_np)
+    _lib.check(_lib.lib().cz_plan_order(d.ctypes.data, count, order.ctypes.data), "cz_plan_order")
+    return order
+
+
+DESC_DTYPE = np.dtype([("in_off", "<u8"), ("out_off", "<u8"), ("len", "<u4"), ("key_idx", "<u4"),
+                       ("counter", "<u8"), ("flags", "<u4"), ("prev", "<i4")])

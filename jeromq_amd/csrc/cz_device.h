@@ -1,0 +1,188 @@
+// cz_device.h -- CDNA4 (gfx950) device primitives for the CurveZMQ MESSAGE path.
+//
+// The arithmetic is the NaCl crypto_box_afternm construction that JeroMQ calls
+// through jnacl (Curve.java:129-147 -> curve25519xsalsa20poly1305.crypto_box_afternm):
+// Salsa20/20 keystream (HSalsa20-derived subkey) XOR + Poly1305 over c[32:mlen].
+// Everything here is plain 32-bit integer VALU work: v_add_u32 / v_alignbit_b32
+// (rotates) / v_xor_b32 for Salsa20, v_mad_u64_u32 chains for Poly1305 in a
+// 2^32 radix.  No MFMA: the path is a stream cipher + a 130-bit MAC.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+namespace cz {
+
+typedef uint32_t u32;
+typedef uint64_t u64;
+
+// "expand 32-byte k"
+constexpr u32 SIGMA0 = 0x61707865u, SIGMA1 = 0x3320646eu, SIGMA2 = 0x79622d32u, SIGMA3 = 0x6b206574u;
+
+__device__ __forceinline__ u32 rotl(u32 v, int c) { return __builtin_amdgcn_alignbit(v, v, 32 - c); }
+
+__device__ __forceinline__ void qr(u32 &a, u32 &b, u32 &c, u32 &d)
+{
+    b ^= rotl(a + d, 7);
+    c ^= rotl(b + a, 9);
+    d ^= rotl(c + b, 13);
+    a ^= rotl(d + c, 18);
+}
+
+__device__ __forceinline__ void double_rounds(u32 x[16])
+{
+#pragma unroll
+    for (int i = 0; i < 10; i++) {
+        qr(x[0], x[4], x[8], x[12]);
+        qr(x[5], x[9], x[13], x[1]);
+        qr(x[10], x[14], x[2], x[6]);
+        qr(x[15], x[3], x[7], x[11]);
+        qr(x[0], x[1], x[2], x[3]);
+        qr(x[5], x[6], x[7], x[4]);
+        qr(x[10], x[11], x[8], x[9]);
+        qr(x[15], x[12], x[13], x[14]);
+    }
+}
+
+// One Salsa20/20 block: key k[8] (LE words), nonce words n0,n1 (LE loads of
+// nonce bytes 16..23 of the XSalsa20 nonce), 64-bit block counter c0|c1.
+__device__ __forceinline__ void salsa20_block(u32 x[16], const u32 k[8], u32 n0, u32 n1, u32 c0, u32 c1)
+{
+    x[0] = SIGMA0; x[1] = k[0]; x[2] = k[1]; x[3] = k[2];
+    x[4] = k[3]; x[5] = SIGMA1; x[6] = n0; x[7] = n1;
+    x[8] = c0; x[9] = c1; x[10] = SIGMA2; x[11] = k[4];
+    x[12] = k[5]; x[13] = k[6]; x[14] = k[7]; x[15] = SIGMA3;
+    double_rounds(x);
+    x[0] += SIGMA0; x[1] += k[0]; x[2] += k[1]; x[3] += k[2];
+    x[4] += k[3]; x[5] += SIGMA1; x[6] += n0; x[7] += n1;
+    x[8] += c0; x[9] += c1; x[10] += SIGMA2; x[11] += k[4];
+    x[12] += k[5]; x[13] += k[6]; x[14] += k[7]; x[15] += SIGMA3;
+}
+
+// HSalsa20(k, in16) -> out[8]: no feed-forward, words 0,5,10,15,6,7,8,9.
+__device__ __forceinline__ void hsalsa20(u32 out[8], const u32 k[8], const u32 in[4])
+{
+    u32 x[16];
+    x[0] = SIGMA0; x[1] = k[0]; x[2] = k[1]; x[3] = k[2];
+    x[4] = k[3]; x[5] = SIGMA1; x[6] = in[0]; x[7] = in[1];
+    x[8] = in[2]; x[9] = in[3]; x[10] = SIGMA2; x[11] = k[4];
+    x[12] = k[5]; x[13] = k[6]; x[14] = k[7]; x[15] = SIGMA3;
+    double_rounds(x);
+    out[0] = x[0]; out[1] = x[5]; out[2] = x[10]; out[3] = x[15];
+    out[4] = x[6]; out[5] = x[7]; out[6] = x[8]; out[7] = x[9];
+}
+
+// ---- Poly1305, radix 2^32 ------------------------------------------------
+// h = h4:h3:h2:h1:h0 (h4 small), r clamped so that r1..r3 have their two low
+// bits clear, hence 2^128 * r_i == (5/4) r_i (mod p) and s_i = r_i + r_i/4 is
+// exact.  Per 16-byte block: 16 + 3 v_mad_u64_u32, one v_mul_lo_u32, and the
+// carry chain.  Bounds: h0..h3 < 2^32, h4 <= 6, r_i < 2^28, s_i < 1.25*2^28,
+// so each 4-term product column is < 2^62.4 and fits a u64.
+struct Poly {
+    u32 h0, h1, h2, h3, h4;
+    u32 r0, r1, r2, r3;
+    u32 s1, s2, s3;
+    u32 p0, p1, p2, p3;
+};
+
+// key = keystream words 0..7 of block 0 (r = words 0..3 clamped, pad = 4..7)
+__device__ __forceinline__ void poly_init(Poly &P, u32 k0, u32 k1, u32 k2, u32 k3, u32 k4, u32 k5, u32 k6, u32 k7)
+{
+    P.r0 = k0 & 0x0fffffffu;
+    P.r1 = k1 & 0x0ffffffcu;
+    P.r2 = k2 & 0x0ffffffcu;
+    P.r3 = k3 & 0x0ffffffcu;
+    P.s1 = P.r1 + (P.r1 >> 2);
+    P.s2 = P.r2 + (P.r2 >> 2);
+    P.s3 = P.r3 + (P.r3 >> 2);
+    P.p0 = k4; P.p1 = k5; P.p2 = k6; P.p3 = k7;
+    P.h0 = P.h1 = P.h2 = P.h3 = P.h4 = 0;
+}
+
+__device__ __forceinline__ void poly_block(Poly &P, u32 m0, u32 m1, u32 m2, u32 m3, u32 hibit)
+{
+    u64 t;
+    t = (u64)P.h0 + m0;
+    u32 h0 = (u32)t;
+    t = (u64)P.h1 + m1 + (t >> 32);
+    u32 h1 = (u32)t;
+    t = (u64)P.h2 + m2 + (t >> 32);
+    u32 h2 = (u32)t;
+    t = (u64)P.h3 + m3 + (t >> 32);
+    u32 h3 = (u32)t;
+    u32 h4 = P.h4 + (u32)(t >> 32) + hibit;
+
+    u64 d0 = (u64)h0 * P.r0 + (u64)h1 * P.s3 + (u64)h2 * P.s2 + (u64)h3 * P.s1;
+    u64 d1 = (u64)h0 * P.r1 + (u64)h1 * P.r0 + (u64)h2 * P.s3 + (u64)h3 * P.s2 + (u64)h4 * P.s1;
+    u64 d2 = (u64)h0 * P.r2 + (u64)h1 * P.r1 + (u64)h2 * P.r0 + (u64)h3 * P.s3 + (u64)h4 * P.s2;
+    u64 d3 = (u64)h0 * P.r3 + (u64)h1 * P.r2 + (u64)h2 * P.r1 + (u64)h3 * P.r0 + (u64)h4 * P.s3;
+    u32 h4r = h4 * P.r0;
+
+    d1 += d0 >> 32;
+    d2 += d1 >> 32;
+    d3 += d2 >> 32;
+    h4 = h4r + (u32)(d3 >> 32);
+    // partial reduction: 2^130 == 5
+    u32 c = (h4 >> 2) + (h4 & ~3u);
+    h4 &= 3u;
+    t = (u64)(u32)d0 + c;
+    P.h0 = (u32)t;
+    t = (u64)(u32)d1 + (t >> 32);
+    P.h1 = (u32)t;
+    t = (u64)(u32)d2 + (t >> 32);
+    P.h2 = (u32)t;
+    t = (u64)(u32)d3 + (t >> 32);
+    P.h3 = (u32)t;
+    P.h4 = h4 + (u32)(t >> 32);
+}
+
+// Final block of len bytes (1..15): bytes >= len cleared, byte len = 0x01, no 2^128 bit.
+__device__ __forceinline__ void poly_block_partial(Poly &P, u32 m0, u32 m1, u32 m2, u32 m3, u32 len)
+{
+    u32 m[4] = {m0, m1, m2, m3};
+#pragma unroll
+    for (int i = 0; i < 4; i++) {
+        int rel = (int)len - 4 * i;  // bytes of this dword that are message
+        u32 keep = rel >= 4 ? 0xffffffffu : (rel <= 0 ? 0u : ((1u << (8 * rel)) - 1u));
+        u32 one = (rel >= 0 && rel < 4) ? (1u << (8 * rel)) : 0u;
+        m[i] = (m[i] & keep) | one;
+    }
+    poly_block(P, m[0], m[1], m[2], m[3], 0u);
+}
+
+// tag = (h mod p + pad) mod 2^128
+__device__ __forceinline__ void poly_finish(const Poly &P, u32 tag[4])
+{
+    u32 h0 = P.h0, h1 = P.h1, h2 = P.h2, h3 = P.h3, h4 = P.h4;
+    u64 t;
+    u32 c = (h4 >> 2) * 5u;
+    h4 &= 3u;
+    t = (u64)h0 + c; h0 = (u32)t;
+    t = (u64)h1 + (t >> 32); h1 = (u32)t;
+    t = (u64)h2 + (t >> 32); h2 = (u32)t;
+    t = (u64)h3 + (t >> 32); h3 = (u32)t;
+    h4 += (u32)(t >> 32);
+    // g = h + 5; if g >= 2^130 then h = g - 2^130
+    t = (u64)h0 + 5u; u32 g0 = (u32)t;
+    t = (u64)h1 + (t >> 32); u32 g1 = (u32)t;
+    t = (u64)h2 + (t >> 32); u32 g2 = (u32)t;
+    t = (u64)h3 + (t >> 32); u32 g3 = (u32)t;
+    u32 g4 = h4 + (u32)(t >> 32);
+    bool ge = (g4 >> 2) != 0;
+    h0 = ge ? g0 : h0; h1 = ge ? g1 : h1; h2 = ge ? g2 : h2; h3 = ge ? g3 : h3;
+    t = (u64)h0 + P.p0; tag[0] = (u32)t;
+    t = (u64)h1 + P.p1 + (t >> 32); tag[1] = (u32)t;
+    t = (u64)h2 + P.p2 + (t >> 32); tag[2] = (u32)t;
+    t = (u64)h3 + P.p3 + (t >> 32); tag[3] = (u32)t;
+}
+
+__device__ __forceinline__ u32 bswap32(u32 v) { return __builtin_bswap32(v); }
+
+// Salsa20 nonce words for a CurveZMQ MESSAGE counter: the nonce tail is
+// BE64(counter) (Wire.putUInt64, Wire.java:124-136) loaded as two LE words.
+__device__ __forceinline__ void counter_nonce(u64 counter, u32 &n0, u32 &n1)
+{
+    n0 = bswap32((u32)(counter >> 32));
+    n1 = bswap32((u32)counter);
+}
+
+}  // namespace cz

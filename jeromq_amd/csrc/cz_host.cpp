@@ -1,0 +1,467 @@
+// cz_host.cpp -- host side of the C-ABI (include/curvezmq_mi355x.h):
+// argument checking, error reporting, per-thread device context for the jnacl
+// drop-ins, host-staged batch contexts.  Every cryptographic byte is computed
+// by the gfx950 kernels in cz_kernels.hip; there is no CPU crypto fallback:
+// without a usable device every entry point fails with CZ_EHIP.
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cstdio>
+#include <cstring>
+#include <numeric>
+#include <string>
+#include <vector>
+
+#include "../../include/curvezmq_mi355x.h"
+#include "cz_internal.h"
+
+extern "C" {
+hipError_t czk_seal_uniform(const void *, uint64_t, void *, uint64_t, uint32_t, uint32_t, const void *, uint64_t,
+                            const uint8_t *, hipStream_t);
+hipError_t czk_seal_desc(const cz_frame_desc *, const uint32_t *, uint32_t, const void *, void *, const void *,
+                         hipStream_t);
+hipError_t czk_open_desc(const cz_frame_desc *, const uint32_t *, uint32_t, const void *, void *, const void *,
+                         uint16_t *, uint64_t *, hipStream_t);
+hipError_t czk_open_uniform(const void *, uint64_t, void *, uint64_t, uint32_t, uint32_t, const void *, uint64_t, int,
+                            uint16_t *, hipStream_t);
+hipError_t czk_box_nacl(const void *, void *, uint32_t, const void *, uint64_t, int, int *, hipStream_t);
+hipError_t czk_subkeys(const void *, void *, uint32_t, const uint8_t *, hipStream_t);
+hipError_t czk_fill(void *, uint64_t, uint64_t, hipStream_t);
+}
+
+namespace czi {
+
+static thread_local std::string g_err;
+
+int fail(int code, const char *fmt, ...)
+{
+    char buf[512];
+    va_list ap;
+    va_start(ap, fmt);
+    vsnprintf(buf, sizeof buf, fmt, ap);
+    va_end(ap);
+    g_err = buf;
+    return code;
+}
+
+int hip_fail(hipError_t e, const char *where)
+{
+    return fail(CZ_EHIP, "%s: %s", where, hipGetErrorString(e));
+}
+
+const uint8_t *prefix_for(int direction)
+{
+    return (const uint8_t *)(direction == CZ_DIR_S2C ? "CurveZMQMESSAGES" : "CurveZMQMESSAGEC");
+}
+
+// ---- DevBuf ----------------------------------------------------------------
+hipError_t DevBuf::reserve(uint64_t bytes)
+{
+    if (bytes <= cap)
+        return hipSuccess;
+    if (ptr)
+        (void)hipFree(ptr);
+    ptr = nullptr;
+    cap = 0;
+    uint64_t want = std::max<uint64_t>(bytes, 4096);
+    hipError_t e = hipMalloc(&ptr, want);
+    if (e == hipSuccess)
+        cap = want;
+    return e;
+}
+
+void DevBuf::release()
+{
+    if (ptr)
+        (void)hipFree(ptr);
+    ptr = nullptr;
+    cap = 0;
+}
+
+hipError_t HostBuf::reserve(uint64_t bytes)
+{
+    if (bytes <= cap)
+        return hipSuccess;
+    if (ptr)
+        (void)hipHostFree(ptr);
+    ptr = nullptr;
+    cap = 0;
+    uint64_t want = std::max<uint64_t>(bytes, 4096);
+    hipError_t e = hipHostMalloc(&ptr, want, hipHostMallocDefault);
+    if (e == hipSuccess)
+        cap = want;
+    return e;
+}
+
+void HostBuf::release()
+{
+    if (ptr)
+        (void)hipHostFree(ptr);
+    ptr = nullptr;
+    cap = 0;
+}
+
+// ---- per-thread single-shot context ----------------------------------------
+struct Single {
+    bool ready = false;
+    hipStream_t stream = nullptr;
+    DevBuf in, out, key, sub, rc;
+    ~Single()
+    {
+        // thread exit: best effort (the runtime may already be torn down at process exit)
+    }
+};
+
+static thread_local Single t_single;
+
+static int single_init()
+{
+    if (t_single.ready)
+        return CZ_OK;
+    int n = 0;
+    hipError_t e = hipGetDeviceCount(&n);
+    if (e != hipSuccess || n == 0)
+        return fail(CZ_EHIP, "no HIP device available (the CURVE path runs only on the GPU)");
+    e = hipStreamCreateWithFlags(&t_single.stream, hipStreamNonBlocking);
+    if (e != hipSuccess)
+        return hip_fail(e, "hipStreamCreate");
+    if ((e = t_single.key.reserve(64)) != hipSuccess || (e = t_single.sub.reserve(64)) != hipSuccess ||
+        (e = t_single.rc.reserve(64)) != hipSuccess)
+        return hip_fail(e, "hipMalloc");
+    t_single.ready = true;
+    return CZ_OK;
+}
+
+// NaCl box/open of one message on the device.
+static int nacl_one(uint8_t *dst, const uint8_t *src, uint64_t len, const uint8_t n[24], const uint8_t k[32],
+                    int open)
+{
+    if (!dst || !src || !n || !k)
+        return -1;
+    if (len < 32 || len > 0xffffffffull)
+        return -1;
+    if (single_init() != CZ_OK)
+        return -1;
+    Single &s = t_single;
+    hipError_t e;
+    if ((e = s.in.reserve(len + 64)) != hipSuccess || (e = s.out.reserve(len + 64)) != hipSuccess) {
+        hip_fail(e, "hipMalloc");
+        return -1;
+    }
+    uint8_t keyblk[32];
+    memcpy(keyblk, k, 32);
+    uint64_t counter = 0;
+    for (int i = 0; i < 8; i++)
+        counter = (counter << 8) | n[16 + i];
+    int rc = -1;
+    // HSalsa20(k, n[0:16]) on the device, then the single-frame kernel
+    if ((e = hipMemcpyAsync(s.key.ptr, keyblk, 32, hipMemcpyHostToDevice, s.stream)) != hipSuccess ||
+        (e = czk_subkeys(s.key.ptr, s.sub.ptr, 1, n, s.stream)) != hipSuccess ||
+        (e = hipMemcpyAsync(s.in.ptr, src, len, hipMemcpyHostToDevice, s.stream)) != hipSuccess ||
+        (e = czk_box_nacl(s.in.ptr, s.out.ptr, (uint32_t)len, s.sub.ptr, counter, open, (int *)s.rc.ptr,
+                          s.stream)) != hipSuccess ||
+        (e = hipMemcpyAsync(&rc, s.rc.ptr, sizeof(int), hipMemcpyDeviceToHost, s.stream)) != hipSuccess ||
+        (e = hipStreamSynchronize(s.stream)) != hipSuccess) {
+        hip_fail(e, "box");
+        return -1;
+    }
+    if (rc != 0)
+        return -1;  // open: tag mismatch, dst untouched (as NaCl)
+    if ((e = hipMemcpyAsync(dst, s.out.ptr, len, hipMemcpyDeviceToHost, s.stream)) != hipSuccess ||
+        (e = hipStreamSynchronize(s.stream)) != hipSuccess) {
+        hip_fail(e, "box D2H");
+        return -1;
+    }
+    return 0;
+}
+
+}  // namespace czi
+
+using namespace czi;
+
+// ---- cz_ctx ----------------------------------------------------------------
+struct cz_ctx {
+    int device = 0;
+    hipStream_t stream = nullptr;
+    DevBuf desc, in, out, status, keys, subkeys;
+    HostBuf hdesc;
+    uint32_t nkeys = 0;
+};
+
+extern "C" {
+
+const char *cz_last_error(void) { return g_err.c_str(); }
+
+const char *cz_version(void) { return "curvezmq-mi355x 0.1 (gfx950)"; }
+
+int cz_device_ok(void)
+{
+    int n = 0;
+    if (hipGetDeviceCount(&n) != hipSuccess || n == 0)
+        return 0;
+    return 1;
+}
+
+int cz_box_afternm(uint8_t *c, const uint8_t *m, uint64_t mlen, const uint8_t n[24], const uint8_t k[32])
+{
+    return nacl_one(c, m, mlen, n, k, 0);
+}
+
+int cz_box_open_afternm(uint8_t *m, const uint8_t *c, uint64_t clen, const uint8_t n[24], const uint8_t k[32])
+{
+    return nacl_one(m, c, clen, n, k, 1);
+}
+
+int cz_secretbox(uint8_t *c, const uint8_t *m, uint64_t mlen, const uint8_t n[24], const uint8_t k[32])
+{
+    return nacl_one(c, m, mlen, n, k, 0);
+}
+
+int cz_secretbox_open(uint8_t *m, const uint8_t *c, uint64_t clen, const uint8_t n[24], const uint8_t k[32])
+{
+    return nacl_one(m, c, clen, n, k, 1);
+}
+
+int cz_subkeys(void *d_subkeys, const void *d_precom, uint32_t nkeys, int direction, void *stream)
+{
+    if (!d_subkeys || !d_precom)
+        return fail(CZ_EINVAL, "cz_subkeys: null pointer");
+    if (direction != CZ_DIR_C2S && direction != CZ_DIR_S2C)
+        return fail(CZ_EINVAL, "cz_subkeys: bad direction %d", direction);
+    hipError_t e = czk_subkeys(d_precom, d_subkeys, nkeys, prefix_for(direction), (hipStream_t)stream);
+    return e == hipSuccess ? CZ_OK : hip_fail(e, "cz_subkeys");
+}
+
+int cz_subkey(uint8_t out[32], const uint8_t k[32], int direction)
+{
+    if (!out || !k)
+        return fail(CZ_EINVAL, "cz_subkey: null pointer");
+    if (direction != CZ_DIR_C2S && direction != CZ_DIR_S2C)
+        return fail(CZ_EINVAL, "cz_subkey: bad direction %d", direction);
+    int rc = single_init();
+    if (rc != CZ_OK)
+        return rc;
+    Single &s = t_single;
+    hipError_t e;
+    if ((e = hipMemcpyAsync(s.key.ptr, k, 32, hipMemcpyHostToDevice, s.stream)) != hipSuccess ||
+        (e = czk_subkeys(s.key.ptr, s.sub.ptr, 1, prefix_for(direction), s.stream)) != hipSuccess ||
+        (e = hipMemcpyAsync(out, s.sub.ptr, 32, hipMemcpyDeviceToHost, s.stream)) != hipSuccess ||
+        (e = hipStreamSynchronize(s.stream)) != hipSuccess)
+        return hip_fail(e, "cz_subkey");
+    return CZ_OK;
+}
+
+int cz_seal_batch(const cz_frame_desc *d_desc, const uint32_t *d_order, uint32_t count, const void *d_in,
+                  void *d_out, const void *d_subkeys, void *stream)
+{
+    if (count && (!d_desc || !d_in || !d_out || !d_subkeys))
+        return fail(CZ_EINVAL, "cz_seal_batch: null pointer");
+    hipError_t e = czk_seal_desc(d_desc, d_order, count, d_in, d_out, d_subkeys, (hipStream_t)stream);
+    return e == hipSuccess ? CZ_OK : hip_fail(e, "cz_seal_batch");
+}
+
+int cz_open_batch(const cz_frame_desc *d_desc, const uint32_t *d_order, uint32_t count, const void *d_in,
+                  void *d_out, const void *d_subkeys, uint16_t *d_status, uint64_t *d_nonces, void *stream)
+{
+    if (count && (!d_desc || !d_in || !d_out || !d_subkeys || !d_status))
+        return fail(CZ_EINVAL, "cz_open_batch: null pointer");
+    hipError_t e =
+        czk_open_desc(d_desc, d_order, count, d_in, d_out, d_subkeys, d_status, d_nonces, (hipStream_t)stream);
+    return e == hipSuccess ? CZ_OK : hip_fail(e, "cz_open_batch");
+}
+
+int cz_seal_uniform(uint32_t count, uint32_t len, const void *d_in, uint64_t in_stride, void *d_out,
+                    uint64_t out_stride, const void *d_subkey, uint64_t counter0, const uint8_t *d_flags8,
+                    void *stream)
+{
+    if (count && (!d_in || !d_out || !d_subkey))
+        return fail(CZ_EINVAL, "cz_seal_uniform: null pointer");
+    if (count > 1 && (in_stride < len || out_stride < (uint64_t)len + CZ_MESSAGE_OVERHEAD))
+        return fail(CZ_EINVAL, "cz_seal_uniform: stride smaller than the frame");
+    if ((uint64_t)len + CZ_MESSAGE_OVERHEAD > 0xffffffffull)
+        return fail(CZ_EINVAL, "cz_seal_uniform: frame too large");
+    hipError_t e = czk_seal_uniform(d_in, in_stride, d_out, out_stride, count, len, d_subkey, counter0, d_flags8,
+                                    (hipStream_t)stream);
+    return e == hipSuccess ? CZ_OK : hip_fail(e, "cz_seal_uniform");
+}
+
+int cz_open_uniform(uint32_t count, uint32_t size, const void *d_in, uint64_t in_stride, void *d_out,
+                    uint64_t out_stride, const void *d_subkey, uint64_t floor0, int check, uint16_t *d_status,
+                    void *stream)
+{
+    if (count && (!d_in || !d_out || !d_subkey || !d_status))
+        return fail(CZ_EINVAL, "cz_open_uniform: null pointer");
+    if (count > 1 && (in_stride < size || (size >= 33 && out_stride < size - 33u)))
+        return fail(CZ_EINVAL, "cz_open_uniform: stride smaller than the frame");
+    hipError_t e = czk_open_uniform(d_in, in_stride, d_out, out_stride, count, size, d_subkey, floor0, check,
+                                    d_status, (hipStream_t)stream);
+    return e == hipSuccess ? CZ_OK : hip_fail(e, "cz_open_uniform");
+}
+
+int cz_plan_order(const cz_frame_desc *h_desc, uint32_t count, uint32_t *h_order)
+{
+    if (count && (!h_desc || !h_order))
+        return fail(CZ_EINVAL, "cz_plan_order: null pointer");
+    std::iota(h_order, h_order + count, 0u);
+    std::stable_sort(h_order, h_order + count,
+                     [h_desc](uint32_t a, uint32_t b) { return h_desc[a].len > h_desc[b].len; });
+    return CZ_OK;
+}
+
+int cz_fill(void *d_buf, uint64_t nbytes, uint64_t seed, void *stream)
+{
+    if (nbytes && !d_buf)
+        return fail(CZ_EINVAL, "cz_fill: null pointer");
+    hipError_t e = czk_fill(d_buf, nbytes, seed, (hipStream_t)stream);
+    return e == hipSuccess ? CZ_OK : hip_fail(e, "cz_fill");
+}
+
+// ---- host-staged contexts ----------------------------------------------------
+int cz_ctx_create(cz_ctx **out, int device)
+{
+    if (!out)
+        return fail(CZ_EINVAL, "cz_ctx_create: null");
+    *out = nullptr;
+    int n = 0;
+    if (hipGetDeviceCount(&n) != hipSuccess || n == 0)
+        return fail(CZ_EHIP, "no HIP device available (the CURVE path runs only on the GPU)");
+    if (device < 0 || device >= n)
+        return fail(CZ_EINVAL, "cz_ctx_create: device %d of %d", device, n);
+    hipError_t e = hipSetDevice(device);
+    if (e != hipSuccess)
+        return hip_fail(e, "hipSetDevice");
+    cz_ctx *c = new cz_ctx();
+    c->device = device;
+    e = hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking);
+    if (e != hipSuccess) {
+        delete c;
+        return hip_fail(e, "hipStreamCreate");
+    }
+    *out = c;
+    return CZ_OK;
+}
+
+void cz_ctx_destroy(cz_ctx *c)
+{
+    if (!c)
+        return;
+    (void)hipSetDevice(c->device);
+    (void)hipStreamSynchronize(c->stream);
+    c->desc.release();
+    c->in.release();
+    c->out.release();
+    c->status.release();
+    c->keys.release();
+    c->subkeys.release();
+    c->hdesc.release();
+    (void)hipStreamDestroy(c->stream);
+    delete c;
+}
+
+int cz_ctx_set_keys(cz_ctx *c, const uint8_t *h_precom, uint32_t nkeys, int direction)
+{
+    if (!c || (nkeys && !h_precom))
+        return fail(CZ_EINVAL, "cz_ctx_set_keys: null");
+    if (direction != CZ_DIR_C2S && direction != CZ_DIR_S2C)
+        return fail(CZ_EINVAL, "cz_ctx_set_keys: bad direction %d", direction);
+    hipError_t e;
+    (void)hipSetDevice(c->device);
+    if ((e = c->keys.reserve(32ull * nkeys)) != hipSuccess || (e = c->subkeys.reserve(32ull * nkeys)) != hipSuccess)
+        return hip_fail(e, "hipMalloc");
+    if ((e = hipMemcpyAsync(c->keys.ptr, h_precom, 32ull * nkeys, hipMemcpyHostToDevice, c->stream)) != hipSuccess ||
+        (e = czk_subkeys(c->keys.ptr, c->subkeys.ptr, nkeys, prefix_for(direction), c->stream)) != hipSuccess ||
+        (e = hipStreamSynchronize(c->stream)) != hipSuccess)
+        return hip_fail(e, "cz_ctx_set_keys");
+    c->nkeys = nkeys;
+    return CZ_OK;
+}
+
+static int ctx_check_desc(const cz_ctx *c, const cz_frame_desc *d, uint32_t count, uint64_t in_bytes,
+                          uint64_t out_bytes, bool seal)
+{
+    for (uint32_t i = 0; i < count; i++) {
+        uint64_t ilen = d[i].len;
+        uint64_t olen = seal ? ilen + CZ_MESSAGE_OVERHEAD : (ilen >= 33 ? ilen - 33 : 0);
+        if (d[i].in_off + ilen > in_bytes || d[i].out_off + olen > out_bytes)
+            return fail(CZ_EINVAL, "frame %u out of the buffer bounds", i);
+        if (d[i].key_idx >= c->nkeys)
+            return fail(CZ_EINVAL, "frame %u: key_idx %u >= %u keys", i, d[i].key_idx, c->nkeys);
+        if (!seal && d[i].prev >= (int32_t)count)
+            return fail(CZ_EINVAL, "frame %u: prev %d out of range", i, d[i].prev);
+    }
+    return CZ_OK;
+}
+
+static int ctx_run(cz_ctx *c, const cz_frame_desc *h_desc, uint32_t count, const void *h_in, uint64_t in_bytes,
+                   void *h_out, uint64_t out_bytes, uint16_t *h_status, bool seal)
+{
+    if (!c || (count && (!h_desc || !h_in || !h_out)))
+        return fail(CZ_EINVAL, "cz_ctx: null pointer");
+    if (!seal && count && !h_status)
+        return fail(CZ_EINVAL, "cz_ctx_open: null status");
+    int rc = ctx_check_desc(c, h_desc, count, in_bytes, out_bytes, seal);
+    if (rc != CZ_OK)
+        return rc;
+    if (count == 0)
+        return CZ_OK;
+    hipError_t e;
+    (void)hipSetDevice(c->device);
+    if ((e = c->desc.reserve(sizeof(cz_frame_desc) * (uint64_t)count)) != hipSuccess ||
+        (e = c->in.reserve(in_bytes + 16)) != hipSuccess || (e = c->out.reserve(out_bytes + 16)) != hipSuccess ||
+        (e = c->status.reserve(sizeof(uint16_t) * (uint64_t)count)) != hipSuccess)
+        return hip_fail(e, "hipMalloc");
+    if ((e = hipMemcpyAsync(c->desc.ptr, h_desc, sizeof(cz_frame_desc) * (uint64_t)count, hipMemcpyHostToDevice,
+                            c->stream)) != hipSuccess ||
+        (e = hipMemcpyAsync(c->in.ptr, h_in, in_bytes, hipMemcpyHostToDevice, c->stream)) != hipSuccess)
+        return hip_fail(e, "H2D");
+    if (seal) {
+        e = czk_seal_desc((const cz_frame_desc *)c->desc.ptr, nullptr, count, c->in.ptr, c->out.ptr, c->subkeys.ptr,
+                          c->stream);
+    } else {
+        if (out_bytes && (e = hipMemsetAsync(c->out.ptr, 0, out_bytes, c->stream)) != hipSuccess)
+            return hip_fail(e, "memset");
+        e = czk_open_desc((const cz_frame_desc *)c->desc.ptr, nullptr, count, c->in.ptr, c->out.ptr, c->subkeys.ptr,
+                          (uint16_t *)c->status.ptr, nullptr, c->stream);
+    }
+    if (e != hipSuccess)
+        return hip_fail(e, "launch");
+    if ((e = hipMemcpyAsync(h_out, c->out.ptr, out_bytes, hipMemcpyDeviceToHost, c->stream)) != hipSuccess)
+        return hip_fail(e, "D2H");
+    if (!seal &&
+        (e = hipMemcpyAsync(h_status, c->status.ptr, sizeof(uint16_t) * (uint64_t)count, hipMemcpyDeviceToHost,
+                            c->stream)) != hipSuccess)
+        return hip_fail(e, "D2H");
+    if ((e = hipStreamSynchronize(c->stream)) != hipSuccess)
+        return hip_fail(e, "sync");
+    return CZ_OK;
+}
+
+int cz_ctx_seal(cz_ctx *c, const cz_frame_desc *h_desc, uint32_t count, const void *h_in, uint64_t in_bytes,
+                void *h_out, uint64_t out_bytes)
+{
+    return ctx_run(c, h_desc, count, h_in, in_bytes, h_out, out_bytes, nullptr, true);
+}
+
+int cz_ctx_open(cz_ctx *c, const cz_frame_desc *h_desc, uint32_t count, const void *h_in, uint64_t in_bytes,
+                void *h_out, uint64_t out_bytes, uint16_t *h_status)
+{
+    return ctx_run(c, h_desc, count, h_in, in_bytes, h_out, out_bytes, h_status, false);
+}
+
+void *cz_host_alloc(uint64_t bytes)
+{
+    void *p = nullptr;
+    if (hipHostMalloc(&p, bytes, hipHostMallocDefault) != hipSuccess) {
+        fail(CZ_ENOMEM, "hipHostMalloc(%llu) failed", (unsigned long long)bytes);
+        return nullptr;
+    }
+    return p;
+}
+
+void cz_host_free(void *p)
+{
+    if (p)
+        (void)hipHostFree(p);
+}
+
+}  // extern "C"

@@ -1,0 +1,318 @@
+// cz_mechanism.cpp -- host-side mirror of JeroMQ's CURVE Mechanism plugin for
+// MESSAGE traffic, with the crypto on the GPU.
+//
+// Mirrors (names, argument meaning and error behaviour):
+//   abstract class Mechanism: Msg encode(Msg) / Msg decode(Msg)     Mechanism.java:202-210
+//   CurveClientMechanism.encode / decode (CONNECTED state)          CurveClientMechanism.java:126-224
+//   CurveServerMechanism.encode / decode (CONNECTED state)          CurveServerMechanism.java:127-224
+// The handshake (HELLO / WELCOME / INITIATE / READY, per connection) is out of
+// scope for this tier: a mechanism is created in the CONNECTED state from the
+// handshake's outputs (cnPrecom, cnNonce, cnPeerNonce).
+//
+// Error behaviour: encode cannot fail (the reference asserts rc == 0,
+// CurveClientMechanism.java:153-154).  decode returns "null" (here CZ_EPROTO)
+// with errno EPROTO and the monitor event the reference raises:
+//   not "\x07MESSAGE"          -> ZMTP_UNEXPECTED_COMMAND            (:168-172)
+//   size < 33                  -> ZMTP_MALFORMED_COMMAND_MESSAGE     (:174-178)
+//   nonce <= cnPeerNonce       -> client: ZMTP_CRYPTOGRAPHIC (:188-191),
+//                                 server: ZMTP_INVALID_SEQUENCE (CurveServerMechanism.java:188-191)
+//   bad tag                    -> ZMTP_CRYPTOGRAPHIC                 (:219-223)
+// cnPeerNonce is updated before the crypto check, as the reference does (:193).
+#include <hip/hip_runtime.h>
+
+#include <cstring>
+#include <vector>
+
+#include "cz_internal.h"
+
+using namespace czi;
+
+namespace jeromq_amd {
+
+class CurveMechanism {
+public:
+    CurveMechanism(bool as_server, const uint8_t precom[32], uint64_t cn_nonce, uint64_t cn_peer_nonce, int device)
+        : as_server_(as_server), cn_nonce_(cn_nonce), cn_peer_nonce_(cn_peer_nonce), device_(device)
+    {
+        memcpy(precom_, precom, 32);
+    }
+
+    ~CurveMechanism()
+    {
+        if (stream_) {
+            (void)hipSetDevice(device_);
+            (void)hipStreamSynchronize(stream_);
+            (void)hipStreamDestroy(stream_);
+        }
+        for (DevBuf *b : {&keys_, &desc_, &in_, &out_, &status_, &nonces_})
+            b->release();
+        for (HostBuf *b : {&hdesc_, &hstatus_, &hnonces_})
+            b->release();
+    }
+
+    int init()
+    {
+        int n = 0;
+        if (hipGetDeviceCount(&n) != hipSuccess || n == 0)
+            return fail(CZ_EHIP, "no HIP device available (the CURVE path runs only on the GPU)");
+        hipError_t e;
+        if ((e = hipSetDevice(device_)) != hipSuccess)
+            return hip_fail(e, "hipSetDevice");
+        if ((e = hipStreamCreateWithFlags(&stream_, hipStreamNonBlocking)) != hipSuccess)
+            return hip_fail(e, "hipStreamCreate");
+        // subkey table: [0] = ours (encode), [1] = peer's (decode); [2..3] precom staging
+        if ((e = keys_.reserve(128)) != hipSuccess)
+            return hip_fail(e, "hipMalloc");
+        uint8_t *k = (uint8_t *)keys_.ptr;
+        const int tx = as_server_ ? CZ_DIR_S2C : CZ_DIR_C2S;
+        const int rx = as_server_ ? CZ_DIR_C2S : CZ_DIR_S2C;
+        if ((e = hipMemcpyAsync(k + 64, precom_, 32, hipMemcpyHostToDevice, stream_)) != hipSuccess ||
+            (e = czk_subkeys(k + 64, k + 0, 1, prefix_for(tx), stream_)) != hipSuccess ||
+            (e = czk_subkeys(k + 64, k + 32, 1, prefix_for(rx), stream_)) != hipSuccess ||
+            (e = hipMemsetAsync(k + 64, 0, 32, stream_)) != hipSuccess ||
+            (e = hipStreamSynchronize(stream_)) != hipSuccess)
+            return hip_fail(e, "subkeys");
+        return CZ_OK;
+    }
+
+    // Mechanism.encode(Msg) for one MESSAGE
+    int64_t encode(const uint8_t *payload, uint64_t n, int msg_flags, uint8_t *out)
+    {
+        uint64_t in_off = 0, out_off = 0;
+        uint32_t len = (uint32_t)n;
+        uint8_t fl = (uint8_t)msg_flags;
+        int rc = encode_batch(1, payload, &in_off, &len, &fl, out, &out_off);
+        return rc == CZ_OK ? (int64_t)(n + CZ_MESSAGE_OVERHEAD) : rc;
+    }
+
+    int encode_batch(uint32_t count, const uint8_t *h_in, const uint64_t *in_off, const uint32_t *len,
+                     const uint8_t *msg_flags, uint8_t *h_out, const uint64_t *out_off)
+    {
+        if (count == 0)
+            return CZ_OK;
+        if (!h_in || !in_off || !len || !h_out || !out_off)
+            return fail(CZ_EINVAL, "encode_batch: null pointer");
+        // device layout: 16-byte aligned frames, packed
+        std::vector<cz_frame_desc> d(count);
+        uint64_t ib = 0, ob = 0;
+        for (uint32_t i = 0; i < count; i++) {
+            d[i].in_off = ib;
+            d[i].out_off = ob;
+            d[i].len = len[i];
+            d[i].key_idx = 0;
+            d[i].counter = cn_nonce_ + i;  // cnNonce++ per message (CurveClientMechanism.java:161)
+            uint32_t f = msg_flags ? msg_flags[i] : 0u;
+            d[i].flags = f & (CZ_MSG_MORE | CZ_MSG_COMMAND);
+            d[i].prev = -1;
+            ib += (len[i] + 15ull) & ~15ull;
+            ob += (len[i] + CZ_MESSAGE_OVERHEAD + 15ull) & ~15ull;
+        }
+        hipError_t e;
+        (void)hipSetDevice(device_);
+        if ((e = desc_.reserve(sizeof(cz_frame_desc) * (uint64_t)count)) != hipSuccess ||
+            (e = in_.reserve(ib + 16)) != hipSuccess || (e = out_.reserve(ob + 16)) != hipSuccess)
+            return hip_fail(e, "hipMalloc");
+        for (uint32_t i = 0; i < count; i++)
+            if (len[i] && (e = hipMemcpyAsync((uint8_t *)in_.ptr + d[i].in_off, h_in + in_off[i], len[i],
+                                              hipMemcpyHostToDevice, stream_)) != hipSuccess)
+                return hip_fail(e, "H2D");
+        if ((e = hipMemcpyAsync(desc_.ptr, d.data(), sizeof(cz_frame_desc) * (uint64_t)count, hipMemcpyHostToDevice,
+                                stream_)) != hipSuccess ||
+            (e = czk_seal_desc((const cz_frame_desc *)desc_.ptr, nullptr, count, in_.ptr, out_.ptr, keys_.ptr,
+                               stream_)) != hipSuccess)
+            return hip_fail(e, "seal");
+        for (uint32_t i = 0; i < count; i++)
+            if ((e = hipMemcpyAsync(h_out + out_off[i], (uint8_t *)out_.ptr + d[i].out_off,
+                                    len[i] + (uint64_t)CZ_MESSAGE_OVERHEAD, hipMemcpyDeviceToHost, stream_)) !=
+                hipSuccess)
+                return hip_fail(e, "D2H");
+        if ((e = hipStreamSynchronize(stream_)) != hipSuccess)
+            return hip_fail(e, "sync");
+        cn_nonce_ += count;
+        return CZ_OK;
+    }
+
+    // Mechanism.decode(Msg) for one MESSAGE body
+    int64_t decode(const uint8_t *body, uint64_t size, uint8_t *out, int *msg_flags, int *event)
+    {
+        uint64_t in_off = 0, out_off = 0;
+        uint32_t sz = (uint32_t)size;
+        uint8_t fl = 0;
+        int32_t failed = -1;
+        if (size > 0xffffffffull)
+            return fail(CZ_EINVAL, "decode: body too large");
+        int rc = decode_batch(1, body, &in_off, &sz, out, &out_off, &fl, &failed, event);
+        if (rc != CZ_OK)
+            return rc;
+        if (failed >= 0)
+            return CZ_EPROTO;
+        if (msg_flags)
+            *msg_flags = fl;
+        return (int64_t)(size - CZ_MESSAGE_OVERHEAD);
+    }
+
+    int decode_batch(uint32_t count, const uint8_t *h_in, const uint64_t *in_off, const uint32_t *size,
+                     uint8_t *h_out, const uint64_t *out_off, uint8_t *msg_flags, int32_t *failed, int *event)
+    {
+        if (failed)
+            *failed = -1;
+        if (event)
+            *event = 0;
+        if (count == 0)
+            return CZ_OK;
+        if (!h_in || !in_off || !size || !h_out || !out_off)
+            return fail(CZ_EINVAL, "decode_batch: null pointer");
+        std::vector<cz_frame_desc> d(count);
+        uint64_t ib = 0, ob = 0;
+        for (uint32_t i = 0; i < count; i++) {
+            d[i].in_off = ib;
+            d[i].out_off = ob;
+            d[i].len = size[i];
+            d[i].key_idx = 1;
+            d[i].counter = cn_peer_nonce_;
+            d[i].flags = CZ_DESC_CHECK_NONCE;
+            d[i].prev = (int32_t)i - 1;  // frames of this connection, in order
+            ib += (size[i] + 15ull) & ~15ull;
+            uint64_t plen = size[i] >= CZ_MESSAGE_OVERHEAD ? size[i] - CZ_MESSAGE_OVERHEAD : 0;
+            ob += (plen + 15ull) & ~15ull;
+        }
+        hipError_t e;
+        (void)hipSetDevice(device_);
+        if ((e = desc_.reserve(sizeof(cz_frame_desc) * (uint64_t)count)) != hipSuccess ||
+            (e = in_.reserve(ib + 16)) != hipSuccess || (e = out_.reserve(ob + 16)) != hipSuccess ||
+            (e = status_.reserve(2ull * count)) != hipSuccess || (e = nonces_.reserve(8ull * count)) != hipSuccess ||
+            (e = hstatus_.reserve(2ull * count)) != hipSuccess || (e = hnonces_.reserve(8ull * count)) != hipSuccess)
+            return hip_fail(e, "alloc");
+        for (uint32_t i = 0; i < count; i++)
+            if (size[i] && (e = hipMemcpyAsync((uint8_t *)in_.ptr + d[i].in_off, h_in + in_off[i], size[i],
+                                               hipMemcpyHostToDevice, stream_)) != hipSuccess)
+                return hip_fail(e, "H2D");
+        if ((e = hipMemcpyAsync(desc_.ptr, d.data(), sizeof(cz_frame_desc) * (uint64_t)count, hipMemcpyHostToDevice,
+                                stream_)) != hipSuccess ||
+            (e = czk_open_desc((const cz_frame_desc *)desc_.ptr, nullptr, count, in_.ptr, out_.ptr, keys_.ptr,
+                               (uint16_t *)status_.ptr, (uint64_t *)nonces_.ptr, stream_)) != hipSuccess ||
+            (e = hipMemcpyAsync(hstatus_.ptr, status_.ptr, 2ull * count, hipMemcpyDeviceToHost, stream_)) !=
+                hipSuccess ||
+            (e = hipMemcpyAsync(hnonces_.ptr, nonces_.ptr, 8ull * count, hipMemcpyDeviceToHost, stream_)) !=
+                hipSuccess ||
+            (e = hipStreamSynchronize(stream_)) != hipSuccess)
+            return hip_fail(e, "open");
+        const uint16_t *st = (const uint16_t *)hstatus_.ptr;
+        const uint64_t *nn = (const uint64_t *)hnonces_.ptr;
+        // deliver in order; the first failure ends the batch (StreamEngine.java:1072-1073 tears the pipe down)
+        uint32_t ok = 0;
+        for (; ok < count; ok++)
+            if ((st[ok] & 0xff) != CZ_STATUS_OK)
+                break;
+        for (uint32_t i = 0; i < ok; i++) {
+            uint64_t plen = size[i] - CZ_MESSAGE_OVERHEAD;
+            if (plen && (e = hipMemcpyAsync(h_out + out_off[i], (uint8_t *)out_.ptr + d[i].out_off, plen,
+                                            hipMemcpyDeviceToHost, stream_)) != hipSuccess)
+                return hip_fail(e, "D2H");
+            if (msg_flags)
+                msg_flags[i] = (uint8_t)(st[i] >> 8);
+        }
+        if ((e = hipStreamSynchronize(stream_)) != hipSuccess)
+            return hip_fail(e, "sync");
+        if (ok)
+            cn_peer_nonce_ = nn[ok - 1];
+        if (ok < count) {
+            int s = st[ok] & 0xff;
+            int ev = 0;
+            switch (s) {
+            case CZ_STATUS_COMMAND: ev = CZ_ZMTP_UNEXPECTED_COMMAND; break;
+            case CZ_STATUS_MALFORMED: ev = CZ_ZMTP_MALFORMED_COMMAND_MESSAGE; break;
+            case CZ_STATUS_SEQUENCE: ev = as_server_ ? CZ_ZMTP_INVALID_SEQUENCE : CZ_ZMTP_CRYPTOGRAPHIC; break;
+            default:
+                ev = CZ_ZMTP_CRYPTOGRAPHIC;
+                cn_peer_nonce_ = nn[ok];  // the nonce passed the replay check before the tag failed
+                break;
+            }
+            if (failed)
+                *failed = (int32_t)ok;
+            if (event)
+                *event = ev;
+        }
+        return CZ_OK;
+    }
+
+    uint64_t nonce() const { return cn_nonce_; }
+    uint64_t peer_nonce() const { return cn_peer_nonce_; }
+
+private:
+    bool as_server_;
+    uint8_t precom_[32];
+    uint64_t cn_nonce_, cn_peer_nonce_;
+    int device_;
+    hipStream_t stream_ = nullptr;
+    DevBuf keys_, desc_, in_, out_, status_, nonces_;
+    HostBuf hdesc_, hstatus_, hnonces_;
+};
+
+}  // namespace jeromq_amd
+
+struct cz_mech {
+    jeromq_amd::CurveMechanism *impl;
+};
+
+extern "C" {
+
+cz_mech *cz_mech_create(int as_server, const uint8_t precom[32], uint64_t cn_nonce, uint64_t cn_peer_nonce, int device)
+{
+    if (!precom) {
+        fail(CZ_EINVAL, "cz_mech_create: null key");
+        return nullptr;
+    }
+    auto *impl = new jeromq_amd::CurveMechanism(as_server != 0, precom, cn_nonce, cn_peer_nonce, device);
+    if (impl->init() != CZ_OK) {
+        delete impl;
+        return nullptr;
+    }
+    return new cz_mech{impl};
+}
+
+void cz_mech_destroy(cz_mech *m)
+{
+    if (!m)
+        return;
+    delete m->impl;
+    delete m;
+}
+
+int64_t cz_mech_encode(cz_mech *m, const uint8_t *payload, uint64_t n, int msg_flags, uint8_t *out)
+{
+    if (!m || (!payload && n) || !out)
+        return fail(CZ_EINVAL, "cz_mech_encode: null pointer");
+    static const uint8_t empty[16] = {0};
+    return m->impl->encode(payload ? payload : empty, n, msg_flags, out);
+}
+
+int64_t cz_mech_decode(cz_mech *m, const uint8_t *body, uint64_t size, uint8_t *out, int *msg_flags, int *event)
+{
+    if (!m || !body || !out)
+        return fail(CZ_EINVAL, "cz_mech_decode: null pointer");
+    return m->impl->decode(body, size, out, msg_flags, event);
+}
+
+int cz_mech_encode_batch(cz_mech *m, uint32_t count, const uint8_t *h_in, const uint64_t *in_off, const uint32_t *len,
+                         const uint8_t *msg_flags, uint8_t *h_out, const uint64_t *out_off)
+{
+    if (!m)
+        return fail(CZ_EINVAL, "cz_mech_encode_batch: null mech");
+    return m->impl->encode_batch(count, h_in, in_off, len, msg_flags, h_out, out_off);
+}
+
+int cz_mech_decode_batch(cz_mech *m, uint32_t count, const uint8_t *h_in, const uint64_t *in_off,
+                         const uint32_t *size, uint8_t *h_out, const uint64_t *out_off, uint8_t *msg_flags,
+                         int32_t *failed, int *event)
+{
+    if (!m)
+        return fail(CZ_EINVAL, "cz_mech_decode_batch: null mech");
+    return m->impl->decode_batch(count, h_in, in_off, size, h_out, out_off, msg_flags, failed, event);
+}
+
+uint64_t cz_mech_nonce(const cz_mech *m) { return m ? m->impl->nonce() : 0; }
+
+uint64_t cz_mech_peer_nonce(const cz_mech *m) { return m ? m->impl->peer_nonce() : 0; }
+
+}  // extern "C"

@@ -332,15 +332,22 @@ uint64_t or_curve_encode(uint8_t *body, const uint8_t *payload, uint64_t n, uint
 /*
  * Mechanism.decode for one MESSAGE body (size bytes).  from_server names the
  * SENDER of the body (1: it was sealed by the server, i.e. we are the client).
- * Returns 0 and fills payload (size-33 bytes), *flags, *nonce; -1 on a bad
- * prefix / short body / failed tag.  The replay check (nonce <= cnPeerNonce)
- * is the caller's: CurveClientMechanism.java:186-193.
+ * Returns 0 and fills payload (size-33 bytes), *flags, *nonce; otherwise
+ *   3 = not a MESSAGE command  (CurveClientMechanism.java:168-172)
+ *   2 = shorter than 33 bytes  (CurveClientMechanism.java:174-178)
+ *   1 = failed tag             (CurveClientMechanism.java:219-223)
+ * The command test is Msgs.startsWith(msg, "MESSAGE", true) (zmq/io/Msgs.java:20-39):
+ * size >= 8, byte 0 == 7, and bytes 1..6 == "MESSAG" -- its loop stops one
+ * character short, so byte 7 is never compared.  Restated as is.
+ * The replay check (nonce <= cnPeerNonce) is the caller's: CurveClientMechanism.java:186-193.
  */
 int or_curve_decode(uint8_t *payload, uint8_t *flags, uint64_t *nonce, const uint8_t *body, uint64_t size,
                     int from_server, const uint8_t k[32])
 {
-    if (size < 33 || memcmp(body, "\x07MESSAGE", 8) != 0)
-        return -1;
+    if (size < 8 || body[0] != 7 || memcmp(body + 1, "MESSAG", 6) != 0)
+        return 3;
+    if (size < 33)
+        return 2;
     uint64_t clen = 16 + size - 16;
     uint8_t *c = (uint8_t *)calloc(clen, 1), *m = (uint8_t *)malloc(clen);
     uint8_t n24[24];
@@ -359,7 +366,7 @@ int or_curve_decode(uint8_t *payload, uint8_t *flags, uint64_t *nonce, const uin
     }
     free(c);
     free(m);
-    return rc;
+    return rc == 0 ? 0 : 1;
 }
 
 /* ---- synthetic input generator shared with the device (counter-based SplitMix64) ---- */

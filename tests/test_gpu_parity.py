@@ -1,0 +1,384 @@
+"""GPU parity: the gfx950 kernels (through the C-ABI) against the golden fixtures and the
+CPU oracle, bit-exact.  Runs on the MI355X box: `pytest -m gpu`.
+
+Cases follow SURVEY.md 8(c): payload sizes {0..65536}, flags 0..3, both directions,
+counters {2, 3, 2^32-1, 2^32, 2^63-1}, tampered tag / ciphertext / header, replay,
+unaligned offsets, ragged batches, and full-size round trips.
+"""
+import ctypes
+import hashlib
+
+import numpy as np
+import pytest
+
+from cz_testlib import (DESC_DTYPE, load_golden, oracle, or_curve_encode, splitmix_bytes, splitmix_words)
+
+pytestmark = pytest.mark.gpu
+
+G = load_golden()
+PRECOM = bytes.fromhex(G["keys"]["precom"])
+
+
+@pytest.fixture(scope="module")
+def torch_dev():
+    import torch
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    return torch, torch.device("cuda:0")
+
+
+@pytest.fixture(scope="module")
+def L():
+    from jeromq_amd import _lib
+    return _lib
+
+
+@pytest.fixture(scope="module")
+def subkeys(torch_dev, L):
+    torch, dev = torch_dev
+    from jeromq_amd import batch
+    k = torch.tensor(list(PRECOM), dtype=torch.uint8, device=dev).view(1, 32)
+    return torch.cat([batch.subkeys(k, L.CZ_DIR_C2S), batch.subkeys(k, L.CZ_DIR_S2C)])
+
+
+def _pack(frames, align=16, base_in=0, base_out=0, overhead=33):
+    """frames: list of (payload bytes, flags, counter, key_idx) -> desc, host input"""
+    desc = np.zeros(len(frames), dtype=DESC_DTYPE)
+    io, oo = base_in, base_out
+    for i, (p, fl, ctr, kidx) in enumerate(frames):
+        desc[i] = (io, oo, len(p), kidx, ctr, fl, -1)
+        io += (len(p) + align - 1) // align * align
+        oo += (len(p) + overhead + align - 1) // align * align
+    hin = np.zeros(max(io + 64, 64), dtype=np.uint8)
+    for i, (p, *_rest) in enumerate(frames):
+        o = int(desc[i]["in_off"])
+        hin[o:o + len(p)] = np.frombuffer(p, dtype=np.uint8)
+    return desc, hin, max(oo + 64, 64)
+
+
+def _seal(torch_dev, subkeys, desc, hin, out_bytes, order=None):
+    torch, dev = torch_dev
+    from jeromq_amd import batch
+    d_in = torch.from_numpy(hin).to(dev)
+    d_out = torch.zeros(out_bytes, dtype=torch.uint8, device=dev)
+    d_desc = torch.from_numpy(desc.view(np.uint8).copy()).to(dev)
+    d_order = None if order is None else torch.from_numpy(order.view(np.int32)).to(dev)
+    batch.seal_batch(d_desc, len(desc), d_in, d_out, subkeys, order=d_order, desc_np=desc)
+    torch.cuda.synchronize()
+    return d_out.cpu().numpy()
+
+
+def test_subkeys_match_golden(subkeys):
+    sk = subkeys.cpu().numpy()
+    assert sk[0].tobytes().hex() == G["keys"]["subkey_c2s"]
+    assert sk[1].tobytes().hex() == G["keys"]["subkey_s2c"]
+
+
+def test_host_subkey(L, torch_dev):
+    from jeromq_amd.curve import subkey
+    assert subkey(PRECOM, L.CZ_DIR_C2S).hex() == G["keys"]["subkey_c2s"]
+    assert subkey(PRECOM, L.CZ_DIR_S2C).hex() == G["keys"]["subkey_s2c"]
+
+
+def test_golden_messages_seal(torch_dev, subkeys):
+    msgs = G["messages"]
+    frames = [(splitmix_bytes(v["n"], v["seed"]), v["flags"], v["counter"], v["from_server"]) for v in msgs]
+    desc, hin, ob = _pack(frames)
+    out = _seal(torch_dev, subkeys, desc, hin, ob)
+    for i, v in enumerate(msgs):
+        o = int(desc[i]["out_off"])
+        body = out[o:o + v["n"] + 33].tobytes()
+        assert hashlib.sha256(body).hexdigest() == v["sha256"], f"vector {i}: {v['n']} B"
+        if "body" in v:
+            assert body.hex() == v["body"]
+
+
+def test_survey_kat(torch_dev, subkeys):
+    kat = G["survey_kat"]
+    desc, hin, ob = _pack([(bytes.fromhex(kat["payload_hex"]), 0, 3, 0)])
+    out = _seal(torch_dev, subkeys, desc, hin, ob)
+    assert out[:133].tobytes().hex() == kat["body"]
+
+
+def _open(torch_dev, subkeys, odesc, hin, out_bytes, nonces=False):
+    torch, dev = torch_dev
+    from jeromq_amd import batch
+    d_in = torch.from_numpy(hin).to(dev)
+    d_out = torch.zeros(out_bytes, dtype=torch.uint8, device=dev)
+    d_desc = torch.from_numpy(odesc.view(np.uint8).copy()).to(dev)
+    status = torch.full((len(odesc),), -1, dtype=torch.int16, device=dev)
+    d_non = torch.zeros(len(odesc), dtype=torch.int64, device=dev) if nonces else None
+    batch.open_batch(d_desc, len(odesc), d_in, d_out, subkeys, status, nonces=d_non, desc_np=odesc)
+    torch.cuda.synchronize()
+    st = status.cpu().numpy().view(np.uint16)
+    return st, d_out.cpu().numpy(), (d_non.cpu().numpy().view(np.uint64) if nonces else None)
+
+
+def _bodies_desc(bodies, key_idx, floors, check=True, align=16):
+    desc = np.zeros(len(bodies), dtype=DESC_DTYPE)
+    io, oo = 0, 0
+    for i, b in enumerate(bodies):
+        desc[i] = (io, oo, len(b), key_idx[i], floors[i], 0x100 if check else 0, -1)
+        io += (len(b) + align - 1) // align * align
+        oo += (max(len(b) - 33, 0) + align - 1) // align * align
+    hin = np.zeros(io + 64, dtype=np.uint8)
+    for i, b in enumerate(bodies):
+        o = int(desc[i]["in_off"])
+        hin[o:o + len(b)] = np.frombuffer(b, dtype=np.uint8)
+    return desc, hin, oo + 64
+
+
+def test_golden_messages_open(torch_dev, subkeys, L):
+    msgs = [v for v in G["messages"] if "body" in v]
+    bodies = [bytes.fromhex(v["body"]) for v in msgs]
+    desc, hin, ob = _bodies_desc(bodies, [v["from_server"] for v in msgs], [v["counter"] - 1 for v in msgs])
+    st, out, nn = _open(torch_dev, subkeys, desc, hin, ob, nonces=True)
+    for i, v in enumerate(msgs):
+        assert st[i] & 0xff == L.CZ_STATUS_OK, f"vector {i}"
+        assert st[i] >> 8 == v["flags"]
+        assert nn[i] == v["counter"]
+        o = int(desc[i]["out_off"])
+        assert out[o:o + v["n"]].tobytes() == splitmix_bytes(v["n"], v["seed"])
+
+
+def test_open_rejections(torch_dev, subkeys, L):
+    v = next(x for x in G["messages"] if x["n"] == 100 and x["from_server"] == 0 and "body" in x)
+    good = bytes.fromhex(v["body"])
+    tag_bad = bytearray(good); tag_bad[20] ^= 1
+    ct_bad = bytearray(good); ct_bad[-1] ^= 0x80
+    flag_bad = bytearray(good); flag_bad[32] ^= 2
+    cmd_bad = b"\x07MESSAXE" + good[8:]
+    quirk = b"\x07MESSAGx" + good[8:]   # Msgs.startsWith never compares byte 7
+    short = good[:32]
+    tiny = good[:7]
+    wrong_dir = good
+    bodies = [good, bytes(tag_bad), bytes(ct_bad), bytes(flag_bad), cmd_bad, quirk, short, tiny, wrong_dir, good, good]
+    keys = [0] * 8 + [1, 0, 0]
+    floors = [v["counter"] - 1] * 9 + [v["counter"], v["counter"] + 5]
+    desc, hin, ob = _bodies_desc(bodies, keys, floors)
+    st, out, _ = _open(torch_dev, subkeys, desc, hin, ob)
+    want = [L.CZ_STATUS_OK, L.CZ_STATUS_CRYPTO, L.CZ_STATUS_CRYPTO, L.CZ_STATUS_CRYPTO, L.CZ_STATUS_COMMAND,
+            L.CZ_STATUS_OK, L.CZ_STATUS_MALFORMED, L.CZ_STATUS_COMMAND, L.CZ_STATUS_CRYPTO, L.CZ_STATUS_SEQUENCE,
+            L.CZ_STATUS_SEQUENCE]
+    assert list(st & 0xff) == want
+    # rejected frames never expose plaintext
+    for i in (1, 2, 3, 8):
+        o = int(desc[i]["out_off"])
+        assert not out[o:o + 100].any()
+    o = int(desc[5]["out_off"])
+    assert out[o:o + 100].tobytes() == splitmix_bytes(100, v["seed"])
+
+
+def test_open_signed_nonce_compare(torch_dev, subkeys, L):
+    # Java compares `long` values: a nonce >= 2^63 is negative and fails against floor 5
+    p = b"x" * 10
+    b1 = or_curve_encode(p, 0, 1 << 63, 0, PRECOM)
+    b2 = or_curve_encode(p, 0, (1 << 63) - 1, 0, PRECOM)
+    desc, hin, ob = _bodies_desc([b1, b2], [0, 0], [5, 5])
+    st, _, _ = _open(torch_dev, subkeys, desc, hin, ob)
+    assert list(st & 0xff) == [L.CZ_STATUS_SEQUENCE, L.CZ_STATUS_OK]
+
+
+def test_open_prev_chain(torch_dev, subkeys, L):
+    bodies = [or_curve_encode(b"abc" * i, 0, c, 0, PRECOM) for i, c in enumerate([3, 4, 9, 9, 10])]
+    desc, hin, ob = _bodies_desc(bodies, [0] * 5, [2] * 5)
+    desc["prev"] = [-1, 0, 1, 2, 3]
+    st, _, _ = _open(torch_dev, subkeys, desc, hin, ob)
+    assert list(st & 0xff) == [0, 0, 0, L.CZ_STATUS_SEQUENCE, 0]
+
+
+@pytest.mark.parametrize("shift", [1, 3, 8])
+def test_unaligned_offsets(torch_dev, subkeys, shift):
+    frames = [(splitmix_bytes(n, 500 + n), n & 3, 1000 + n, n & 1) for n in [0, 5, 31, 32, 33, 64, 100, 257, 4096]]
+    desc, hin, ob = _pack(frames, align=16)
+    desc["in_off"] += shift
+    desc["out_off"] += 2 * shift + 1
+    hin = np.concatenate([np.zeros(shift, dtype=np.uint8), hin])
+    out = _seal(torch_dev, subkeys, desc, hin, ob + 64)
+    for i, (p, fl, ctr, k) in enumerate(frames):
+        o = int(desc[i]["out_off"])
+        assert out[o:o + len(p) + 33].tobytes() == or_curve_encode(p, fl, ctr, k, PRECOM)
+    # and open from unaligned bodies
+    bodies = [or_curve_encode(p, fl, ctr, k, PRECOM) for (p, fl, ctr, k) in frames]
+    odesc, ohin, oob = _bodies_desc(bodies, [f[3] for f in frames], [f[2] - 1 for f in frames])
+    odesc["in_off"] += shift
+    odesc["out_off"] += 3
+    ohin = np.concatenate([np.zeros(shift, dtype=np.uint8), ohin])
+    st, pout, _ = _open(torch_dev, subkeys, odesc, ohin, oob + 16)
+    assert not np.any(st & 0xff)
+    for i, (p, *_r) in enumerate(frames):
+        o = int(odesc[i]["out_off"])
+        assert pout[o:o + len(p)].tobytes() == p
+
+
+def _oracle_seal(desc, hin, out_bytes, from_server=0):
+    out = np.zeros(out_bytes, dtype=np.uint8)
+    precom = np.frombuffer(PRECOM * 2, dtype=np.uint8)
+    oracle().or_seal_batch(desc.ctypes.data, len(desc), hin.ctypes.data, out.ctypes.data, precom.ctypes.data,
+                           from_server, 8)
+    return out
+
+
+def test_ragged_zipf_vs_oracle(torch_dev, subkeys):
+    rng = np.random.default_rng(42)
+    n = 3000
+    j = rng.zipf(1.2, size=n)
+    j = np.clip(j, 1, 1024)
+    lens = (64 * j - rng.integers(0, 64, size=n)).astype(np.uint32)  # ragged, not multiples of 64
+    frames = [(splitmix_bytes(int(l), 9000 + i), i & 3, 3 + i, 0) for i, l in enumerate(lens)]
+    desc, hin, ob = _pack(frames)
+    from jeromq_amd.batch import plan_order
+    order = plan_order(desc)
+    out = _seal(torch_dev, subkeys, desc, hin, ob, order=order)
+    want = _oracle_seal(desc, hin, ob)
+    assert np.array_equal(out, want)
+
+
+def test_uniform_4k_vs_oracle_and_roundtrip(torch_dev, subkeys, L):
+    torch, dev = torch_dev
+    from jeromq_amd import batch
+    count, n = 4096, 4096
+    in_stride, out_stride = 4096, 4144
+    d_in = torch.empty(count * in_stride, dtype=torch.uint8, device=dev)
+    batch.fill(d_in, 0x5EED0002)
+    flags = torch.zeros(count, dtype=torch.uint8, device=dev)
+    flags[::8] = 1
+    d_out = torch.zeros(count * out_stride, dtype=torch.uint8, device=dev)
+    batch.seal_uniform(d_in, in_stride, d_out, out_stride, count, n, subkeys[0], 3, flags8=flags)
+    torch.cuda.synchronize()
+    hin = d_in.cpu().numpy()
+    assert hin[:64].tobytes() == splitmix_words(8, 0x5EED0002).view(np.uint8).tobytes()
+    desc = np.zeros(count, dtype=DESC_DTYPE)
+    desc["in_off"] = np.arange(count, dtype=np.uint64) * in_stride
+    desc["out_off"] = np.arange(count, dtype=np.uint64) * out_stride
+    desc["len"] = n
+    desc["counter"] = 3 + np.arange(count, dtype=np.uint64)
+    desc["flags"] = flags.cpu().numpy()
+    want = _oracle_seal(desc, hin, count * out_stride)
+    got = d_out.cpu().numpy()
+    for i in range(count):
+        o = i * out_stride
+        assert got[o:o + n + 33].tobytes() == want[o:o + n + 33].tobytes(), f"frame {i}"
+    # open back, in order, replay-checked
+    d_plain = torch.zeros(count * in_stride, dtype=torch.uint8, device=dev)
+    status = torch.full((count,), -1, dtype=torch.int16, device=dev)
+    batch.open_uniform(d_out, out_stride, d_plain, in_stride, count, n + 33, subkeys[0], 2, status)
+    torch.cuda.synchronize()
+    st = status.cpu().numpy().view(np.uint16)
+    assert np.all(st & 0xff == 0)
+    assert np.array_equal(st >> 8, flags.cpu().numpy())
+    assert torch.equal(d_plain, d_in)
+
+
+def test_nacl_box_afternm_golden(L, torch_dev):
+    from jeromq_amd.curve import Curve
+    cv = Curve()
+    for v in G["box_afternm"]:
+        key, n24 = bytes.fromhex(v["key"]), bytes.fromhex(v["nonce"])
+        m = bytes(32) + splitmix_bytes(v["n"], v["m_seed"])
+        c = bytearray(len(m))
+        assert cv.afternm(c, m, len(m), n24, key) == 0
+        assert c.hex() == v["c"]
+        m2 = bytearray(len(m))
+        assert cv.openAfternm(m2, bytes(c), len(c), n24, key) == 0
+        assert bytes(m2) == m
+        c[-1] ^= 1
+        m3 = bytearray(len(m))
+        assert cv.openAfternm(m3, bytes(c), len(c), n24, key) == -1
+        assert not any(m3)
+    assert cv.afternm(bytearray(31), bytes(31), 31, bytes(24), bytes(32)) == -1
+
+
+def test_mechanism_client_server(L, torch_dev):
+    from jeromq_amd.mechanism import CurveClientMechanism, CurveServerMechanism, Msg
+    cli = CurveClientMechanism(PRECOM)
+    srv = CurveServerMechanism(PRECOM)
+    payloads = [splitmix_bytes(n, 40 + n) for n in (0, 1, 32, 100, 4096, 70000)]
+    for i, p in enumerate(payloads):
+        enc = cli.encode(Msg(p, i & 3))
+        assert enc.data == or_curve_encode(p, i & 3, 3 + i, 0, PRECOM)
+        dec = srv.decode(enc)
+        assert dec is not None and dec.data == p and dec.flags == i & 3
+    assert cli.cnNonce == 3 + len(payloads) and srv.cnPeerNonce == 2 + len(payloads)
+    # replay: the same body again is an INVALID_SEQUENCE on the server ...
+    again = cli.encode(Msg(b"hello"))
+    assert srv.decode(again) is not None
+    assert srv.decode(again) is None and srv.last_event == L.CZ_ZMTP_INVALID_SEQUENCE
+    # ... and CRYPTOGRAPHIC on the client (CurveClientMechanism.java:188-191)
+    back = srv.encode(Msg(b"pong", Msg.MORE))
+    assert cli.decode(back).data == b"pong"
+    assert cli.decode(back) is None and cli.last_event == L.CZ_ZMTP_CRYPTOGRAPHIC
+    bad = bytearray(srv.encode(Msg(b"tamper")).data)
+    bad[-1] ^= 1
+    assert cli.decode(Msg(bytes(bad))) is None and cli.last_event == L.CZ_ZMTP_CRYPTOGRAPHIC
+    assert cli.decode(Msg(b"\x07MESSAGE" + bytes(10))) is None
+    assert cli.last_event == L.CZ_ZMTP_MALFORMED_COMMAND_MESSAGE
+    assert cli.decode(Msg(b"\x05READY" + bytes(40))) is None and cli.last_event == L.CZ_ZMTP_UNEXPECTED_COMMAND
+
+
+def test_mechanism_batches(L, torch_dev):
+    from jeromq_amd.mechanism import CurveClientMechanism, CurveServerMechanism, Msg
+    cli = CurveClientMechanism(PRECOM)
+    srv = CurveServerMechanism(PRECOM)
+    msgs = [Msg(splitmix_bytes(n, n), n & 1) for n in range(0, 300, 7)]
+    enc = cli.encodeBatch(msgs)
+    for i, (m, e) in enumerate(zip(msgs, enc)):
+        assert e.data == or_curve_encode(m.data, m.flags, 3 + i, 0, PRECOM)
+    enc[20] = Msg(enc[20].data[:-1] + bytes([enc[20].data[-1] ^ 1]))
+    dec = srv.decodeBatch(enc)
+    assert len(dec) == 20 and all(d.data == m.data and d.flags == m.flags for d, m in zip(dec, msgs))
+    assert srv.last_event == L.CZ_ZMTP_CRYPTOGRAPHIC
+
+
+def test_ctx_host_staged(L, torch_dev):
+    lib = L.lib()
+    ctx = ctypes.c_void_p()
+    L.check(lib.cz_ctx_create(ctypes.byref(ctx), 0))
+    try:
+        L.check(lib.cz_ctx_set_keys(ctx, PRECOM, 1, L.CZ_DIR_S2C))
+        frames = [(splitmix_bytes(n, 3 * n), 1, 2 + i, 0) for i, n in enumerate([0, 10, 100, 1000, 5000])]
+        desc, hin, ob = _pack(frames)
+        hout = np.zeros(ob, dtype=np.uint8)
+        L.check(lib.cz_ctx_seal(ctx, desc.ctypes.data, len(desc), hin.ctypes.data, hin.nbytes, hout.ctypes.data,
+                                hout.nbytes))
+        for i, (p, fl, ctr, k) in enumerate(frames):
+            o = int(desc[i]["out_off"])
+            assert hout[o:o + len(p) + 33].tobytes() == or_curve_encode(p, fl, ctr, 1, PRECOM)
+        # out-of-bounds descriptor is rejected before any launch
+        bad = desc.copy()
+        bad["in_off"][0] = hin.nbytes
+        bad["len"][0] = 1
+        assert lib.cz_ctx_seal(ctx, bad.ctypes.data, len(bad), hin.ctypes.data, hin.nbytes, hout.ctypes.data,
+                               hout.nbytes) == L.CZ_EINVAL
+    finally:
+        lib.cz_ctx_destroy(ctx)
+
+
+@pytest.mark.parametrize("count,n", [(1 << 20, 100), (1 << 20, 4096)])
+def test_full_size_roundtrip(torch_dev, subkeys, count, n):
+    """BASELINE configs 2 and 3 at full size: seal -> open round trip, sampled frames vs oracle."""
+    torch, dev = torch_dev
+    from jeromq_amd import batch
+    in_stride = (n + 15) // 16 * 16
+    out_stride = (n + 33 + 15) // 16 * 16
+    d_in = torch.empty(count * in_stride, dtype=torch.uint8, device=dev)
+    batch.fill(d_in, 0x5EED0000 + n)
+    d_out = torch.empty(count * out_stride, dtype=torch.uint8, device=dev)
+    batch.seal_uniform(d_in, in_stride, d_out, out_stride, count, n, subkeys[0], 3)
+    d_plain = torch.zeros_like(d_in)
+    status = torch.full((count,), -1, dtype=torch.int16, device=dev)
+    batch.open_uniform(d_out, out_stride, d_plain, in_stride, count, n + 33, subkeys[0], 2, status)
+    torch.cuda.synchronize()
+    assert int((status != 0).sum()) == 0
+    if in_stride == n:
+        assert torch.equal(d_plain, d_in)
+    else:
+        assert torch.equal(d_plain.view(count, in_stride)[:, :n], d_in.view(count, in_stride)[:, :n])
+    rng = np.random.default_rng(n)
+    for i in list(rng.integers(0, count, size=64)) + [0, count - 1]:
+        i = int(i)
+        p = d_in[i * in_stride:i * in_stride + n].cpu().numpy().tobytes()
+        body = d_out[i * out_stride:i * out_stride + n + 33].cpu().numpy().tobytes()
+        assert body == or_curve_encode(p, 0, 3 + i, 0, PRECOM), f"frame {i}"
+    del d_in, d_out, d_plain
+    torch.cuda.empty_cache()

@@ -69,7 +69,7 @@ def test_curve_message(v):
     rc, p2, flags, nonce = or_curve_decode(body, v["from_server"], K)
     assert rc == 0 and p2 == payload and flags == v["flags"] and nonce == v["counter"]
     # wrong direction prefix -> cryptographic failure
-    assert or_curve_decode(body, 1 - v["from_server"], K)[0] == -1
+    assert or_curve_decode(body, 1 - v["from_server"], K)[0] == 1
 
 
 def test_survey_kat():
@@ -82,6 +82,13 @@ def test_survey_kat():
 
 def test_decode_rejects_malformed():
     body = or_curve_encode(b"hello", 0, 3, 0, K)
-    assert or_curve_decode(body[:32], 0, K)[0] == -1
-    bad = b"\x07MESSAGF" + body[8:]
-    assert or_curve_decode(bad, 0, K)[0] == -1
+    assert or_curve_decode(body[:32], 0, K)[0] == 2          # MALFORMED_COMMAND_MESSAGE
+    assert or_curve_decode(body[:7], 0, K)[0] == 3           # too short to be a command
+    assert or_curve_decode(b"\x07MESSAXE" + body[8:], 0, K)[0] == 3   # UNEXPECTED_COMMAND
+    assert or_curve_decode(b"\x08MESSAGE" + body[8:], 0, K)[0] == 3
+    # Msgs.startsWith never compares the 7th character (zmq/io/Msgs.java:31): accepted
+    rc, payload, _, _ = or_curve_decode(b"\x07MESSAGx" + body[8:], 0, K)
+    assert rc == 0 and payload == b"hello"
+    bad = bytearray(body)
+    bad[20] ^= 1
+    assert or_curve_decode(bytes(bad), 0, K)[0] == 1

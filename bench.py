@@ -97,7 +97,9 @@ class Workload:
             n = 4096 if cfg != "100b" else 100
             self.n = n
             self.in_stride = (n + 15) // 16 * 16
-            self.out_stride = (n + 33 + 15) // 16 * 16
+            # 4 KiB: 128-byte body slots (full-line LDS-staged stores); 100 B: dense 16-byte slots
+            # (64 slots fit the LDS region stager)
+            self.out_stride = (n + 33 + 127) // 128 * 128 if n >= 1024 else (n + 33 + 15) // 16 * 16
             self.d_in = torch.empty(frames * self.in_stride, dtype=torch.uint8, device=dev)
             batch.fill(self.d_in, seed)
             self.flags = torch.zeros(frames, dtype=torch.uint8, device=dev)

@@ -121,12 +121,18 @@ int cz_open_batch(const cz_frame_desc *d_desc, const uint32_t *d_order, uint32_t
                   void *d_out, const void *d_subkeys, uint16_t *d_status, uint64_t *d_nonces, void *stream);
 
 /* Uniform-length batch of ONE connection direction: frame i at in + i*in_stride,
- * body i at out + i*out_stride, nonce counter0 + i, flags d_flags8[i] (NULL = 0). */
+ * body i at out + i*out_stride, nonce counter0 + i, flags d_flags8[i] (NULL = 0).
+ * The batch owns count * out_stride output bytes: slot bytes past a body are
+ * written as zero (this lets the kernel store whole 128-byte lines; an
+ * out_stride that is a multiple of 128 -- or 64 slots <= 16 KiB -- takes the
+ * LDS-staged full-line store path). */
 int cz_seal_uniform(uint32_t count, uint32_t len, const void *d_in, uint64_t in_stride, void *d_out,
                     uint64_t out_stride, const void *d_subkey, uint64_t counter0, const uint8_t *d_flags8,
                     void *stream);
 /* Open `count` bodies of `size` bytes of one connection in order; frame 0 must
- * beat floor0, frame i must beat frame i-1 (when check != 0). */
+ * beat floor0, frame i must beat frame i-1 (when check != 0).  Payload i goes to
+ * out + i*out_stride; the batch owns count * out_stride output bytes (slot bytes
+ * past a payload, and rejected frames' slots, are written as zero). */
 int cz_open_uniform(uint32_t count, uint32_t size, const void *d_in, uint64_t in_stride, void *d_out,
                     uint64_t out_stride, const void *d_subkey, uint64_t floor0, int check, uint16_t *d_status,
                     void *stream);

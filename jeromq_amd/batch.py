@@ -39,10 +39,15 @@ def subkeys(precom, direction, stream=None):
 
 
 def seal_uniform(inp, in_stride, out, out_stride, count, length, subkey, counter0, flags8=None, stream=None):
+    """Seal `count` payloads of `length` bytes (frame i at in[i*in_stride]) into MESSAGE
+    bodies; body i goes to slot i = out[i*out_stride : (i+1)*out_stride].  The batch owns
+    whole slots: slot bytes past the body are written (as zeros)."""
     _need_cuda_u8(inp, "in")
     _need_cuda_u8(out, "out")
     need_in = (count - 1) * in_stride + length if count else 0
-    need_out = (count - 1) * out_stride + length + _lib.CZ_MESSAGE_OVERHEAD if count else 0
+    need_out = count * out_stride if count else 0
+    if out_stride < length + _lib.CZ_MESSAGE_OVERHEAD and count > 1:
+        raise ValueError("out_stride smaller than a MESSAGE body")
     if inp.numel() < need_in or out.numel() < need_out:
         raise ValueError("buffer too small for the batch")
     if flags8 is not None and flags8.numel() < count:
@@ -52,12 +57,14 @@ def seal_uniform(inp, in_stride, out, out_stride, count, length, subkey, counter
 
 
 def open_uniform(inp, in_stride, out, out_stride, count, size, subkey, floor0, status, check=True, stream=None):
+    """Open `count` bodies of `size` bytes of one connection, in order; payload i goes to
+    slot out[i*out_stride : (i+1)*out_stride] (whole slots owned by the batch)."""
     _need_cuda_u8(inp, "in")
     _need_cuda_u8(out, "out")
     if count and (inp.numel() < (count - 1) * in_stride + size or status.numel() < count):
         raise ValueError("buffer too small for the batch")
-    if count and size >= 33 and out.numel() < (count - 1) * out_stride + size - 33:
-        raise ValueError("output too small for the batch")
+    if count and size >= 33 and out.numel() < count * out_stride:
+        raise ValueError("output too small for the batch (needs count * out_stride bytes)")
     _lib.check(_lib.lib().cz_open_uniform(count, size, _ptr(inp), in_stride, _ptr(out), out_stride, _ptr(subkey),
                                           floor0, 1 if check else 0, _ptr(status), _stream(stream)),
                "cz_open_uniform")

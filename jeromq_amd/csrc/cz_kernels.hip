@@ -9,16 +9,27 @@
 //     -> Curve.openAfternm (Curve.java:139-147) -> jnacl crypto_box_open_afternm
 //
 // Work mapping: ONE FRAME PER LANE.  A lane walks its frame's Salsa20 blocks in
-// order, keeps the 64-byte block state in VGPRs and accumulates Poly1305 with
-// a serial Horner chain -- so there are no cross-lane reductions and no r^k
-// power tables (Poly1305's key is different for every frame, so a power table
-// would never amortise).  Frames of a wave are independent, so a uniform batch
-// runs divergence-free.  Memory: each lane streams 64 B per step through four
-// 16-byte loads/stores; the 33-byte MESSAGE header shift (flag byte + 32-byte
-// NaCl zero prefix) is absorbed with v_alignbyte_b32 funnel shifts and a
-// 1-dword (seal) / 4-dword (open) carry, so every global access is a 16-byte
-// aligned dwordx4 when the frame offsets are 16-byte aligned (the fast path);
-// other alignments take a byte-wise path with identical results.
+// order with the 64-byte block state in VGPRs and runs Poly1305 as a serial
+// Horner chain, so there are no cross-lane reductions and no r^k tables (the
+// Poly1305 key differs per frame, a power table would never amortise).
+//
+// Memory (measured on MI355X, tools/diag): lane-wise 16-byte loads stream at
+// ~4.9 TB/s, but lane-wise 16-byte STORES reach only ~2.8 TB/s because every
+// 128-byte line is written piecewise; a store instruction that writes whole,
+// aligned 128-byte lines reaches ~4.5 TB/s.  So loads stay lane-wise and the
+// output is staged through LDS by an "emitter":
+//   EmitLines  (large frames, slot stride % 128 == 0): each lane writes its
+//              64-byte chunks into an 8 KiB per-wave LDS line buffer; every 2
+//              chunks the wave flushes one full line per frame, 8 frames per
+//              store instruction (XOR-swizzled, bank-conflict free both ways);
+//   EmitRegion (small frames, 64 slots <= 16 KiB): the wave's whole output
+//              region is assembled in LDS and stored with 1 KiB contiguous
+//              store instructions;
+//   EmitDirect byte-exact per-lane stores (descriptor batches, partial waves,
+//              unaligned frames).
+// The 33-byte MESSAGE header shift (flags byte + 32-byte NaCl zero prefix) is
+// absorbed with v_alignbyte_b32 funnel shifts and a 1-dword (seal) / 8-dword
+// (open) carry.
 //
 // Layout (box coordinates, mlen = 33 + n for a MESSAGE):
 //   box[0:32]   = NaCl ZEROBYTES (keystream bytes 0..31 are the Poly1305 key)
@@ -39,6 +50,11 @@ enum Mode { MODE_ZMQ = 0, MODE_NACL = 1 };
 
 // "\x07MESSAGE" as two little-endian words
 constexpr u32 HDR0 = 0x53454d07u, HDR1 = 0x45474153u;
+
+constexpr int BLOCK = 256;              // threads per workgroup (4 waves)
+constexpr int WAVES = BLOCK / 64;
+constexpr u32 LINE_LDS_BYTES = 64 * 128; // EmitLines: one 128-byte line per frame
+constexpr u32 REGION_MAX = 16384;       // EmitRegion: 64 slots per wave
 
 struct V4 {
     u32 x, y, z, w;
@@ -101,52 +117,215 @@ __device__ __forceinline__ void st_bytes(uint8_t *__restrict__ p, u32 a, u32 b, 
 
 __device__ __forceinline__ u32 funnel(u32 hi, u32 lo, u32 sh) { return __builtin_amdgcn_alignbyte(hi, lo, sh); }
 
-// MAC + store the 16-byte sub-blocks j in [j0, 4) of box block blk whose box
-// bytes are < valid (relative to the block start).  Used for every block that
-// is not a full 64-byte block, and for block 0's ciphertext half.
-template <bool AL>
-__device__ __forceinline__ void emit_guarded(Poly &P, const u32 C[16], int j0, u32 valid, uint8_t *__restrict__ dst,
-                                             bool store)
+// keep the first `valid` bytes (0..64) of a 64-byte chunk, zero the rest
+__device__ __forceinline__ void mask_chunk(u32 D[16], u32 valid)
 {
 #pragma unroll
-    for (int j = 0; j < 4; j++) {
-        if (j < j0)
-            continue;
-        u32 s = 16u * j;
-        if (s >= valid)
-            continue;
-        u32 nb = valid - s;
-        if (nb >= 16) {
-            poly_block(P, C[4 * j], C[4 * j + 1], C[4 * j + 2], C[4 * j + 3], 1u);
-            if (store)
-                st16<AL>(dst + s, C[4 * j], C[4 * j + 1], C[4 * j + 2], C[4 * j + 3]);
-        } else {
-            poly_block_partial(P, C[4 * j], C[4 * j + 1], C[4 * j + 2], C[4 * j + 3], nb);
-            if (store)
-                st_bytes(dst + s, C[4 * j], C[4 * j + 1], C[4 * j + 2], C[4 * j + 3], nb);
-        }
+    for (int k = 0; k < 16; k++) {
+        int rel = (int)valid - 4 * k;
+        u32 keep = rel >= 4 ? 0xffffffffu : (rel <= 0 ? 0u : ((1u << (8 * rel)) - 1u));
+        D[k] &= keep;
     }
 }
 
+// ---------------------------------------------------------------------------
+// Emitters.  A frame's output arrives as 64-byte chunks q = 0, 1, 2, ... (bytes
+// [64q, 64q+64) of the output object, `total` bytes long).  Bytes >= total in
+// the last chunk are don't-care in D.  tag() (seal only) writes output bytes
+// 16..31 after the chunk stream; chunk 0 carries zeros there.
+// ---------------------------------------------------------------------------
+template <bool AL>
+struct EmitDirect {
+    static constexpr bool cooperative = false;
+    uint8_t *dst;
+    u32 total;
+
+    __device__ __forceinline__ void emit(u32 q, const u32 D[16])
+    {
+        const u32 base = 64u * q;
+        uint8_t *p = dst + base;
+        if (base + 64u <= total) {
+            st16<AL>(p, D[0], D[1], D[2], D[3]);
+            st16<AL>(p + 16, D[4], D[5], D[6], D[7]);
+            st16<AL>(p + 32, D[8], D[9], D[10], D[11]);
+            st16<AL>(p + 48, D[12], D[13], D[14], D[15]);
+        } else {
+#pragma unroll
+            for (int c = 0; c < 4; c++) {
+                u32 s = base + 16u * c;
+                if (s < total) {
+                    u32 nb = total - s;
+                    if (nb >= 16)
+                        st16<AL>(dst + s, D[4 * c], D[4 * c + 1], D[4 * c + 2], D[4 * c + 3]);
+                    else
+                        st_bytes(dst + s, D[4 * c], D[4 * c + 1], D[4 * c + 2], D[4 * c + 3], nb);
+                }
+            }
+        }
+    }
+    __device__ __forceinline__ void tag(const u32 t[4]) { st16<AL>(dst + 16, t[0], t[1], t[2], t[3]); }
+    __device__ __forceinline__ void finish() {}
+    __device__ __forceinline__ void close(bool bad)
+    {
+        if (bad)
+            poison();
+    }
+    __device__ void poison()
+    {
+        for (u32 o = 0; o < total; o += 16) {
+            u32 nb = total - o < 16 ? total - o : 16;
+            if (nb == 16)
+                st16<AL>(dst + o, 0u, 0u, 0u, 0u);
+            else
+                st_bytes(dst + o, 0u, 0u, 0u, 0u, nb);
+        }
+    }
+};
+
+// Whole-line staging for a full wave of equal-length frames whose slots are
+// 128-byte multiples (stride % 128 == 0, base 16-byte aligned).  Each frame
+// owns its slot: bytes of the last line beyond `total` are written as zero.
+struct EmitLines {
+    static constexpr bool cooperative = true;  // every lane of the wave must run the same chunk sequence
+    uint4 *lds;        // this wave's 64 x 8 chunks
+    uint8_t *wbase;    // slot of frame 0 of this wave
+    uint8_t *mine;     // this lane's slot
+    u64 stride;
+    u32 lane, total, last_q;
+    bool tag_slot;     // seal: leave bytes 16..31 of line 0 to tag()
+
+    __device__ __forceinline__ void flush(u32 line)
+    {
+        const u32 c = lane & 7u;
+        const u32 r = lane >> 3;
+        uint8_t *p = wbase + (u64)r * stride + 128ull * line + 16u * c;
+        const u64 step = 8ull * stride;
+        const bool skip = tag_slot && line == 0 && c == 1;
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // the other lanes' ds_writes of this line
+#pragma unroll
+        for (u32 j = 0; j < 8; j++) {
+            const u32 F = 8u * j + r;
+            uint4 v = lds[F * 8u + (c ^ (F & 7u))];
+            if (!skip)
+                *reinterpret_cast<uint4 *>(p) = v;
+            p += step;
+        }
+    }
+    __device__ __forceinline__ void emit(u32 q, const u32 Din[16])
+    {
+        u32 D[16];
+#pragma unroll
+        for (int k = 0; k < 16; k++)
+            D[k] = Din[k];
+        if (64u * q + 64u > total)
+            mask_chunk(D, total > 64u * q ? total - 64u * q : 0u);
+        const u32 h = q & 1u;
+        const u32 sw = lane & 7u;
+#pragma unroll
+        for (u32 c = 0; c < 4; c++)
+            lds[lane * 8u + ((4u * h + c) ^ sw)] = make_uint4(D[4 * c], D[4 * c + 1], D[4 * c + 2], D[4 * c + 3]);
+        if (h)
+            flush(q >> 1);
+        last_q = q;
+    }
+    __device__ __forceinline__ void tag(const u32 t[4])
+    {
+        *reinterpret_cast<uint4 *>(mine + 16) = make_uint4(t[0], t[1], t[2], t[3]);
+    }
+    __device__ __forceinline__ void finish()
+    {
+        if ((last_q & 1u) == 0) {
+            const u32 sw = lane & 7u;
+#pragma unroll
+            for (u32 c = 4; c < 8; c++)
+                lds[lane * 8u + (c ^ sw)] = make_uint4(0u, 0u, 0u, 0u);
+            flush(last_q >> 1);
+        }
+    }
+    // converged: flush the last line, then zero rejected frames' slots
+    __device__ __forceinline__ void close(bool bad)
+    {
+        finish();
+        if (bad)
+            poison();
+    }
+    __device__ void poison()
+    {
+        // the plaintext already left through other lanes' stores: make this lane's zeros land after them
+        __threadfence_block();
+        for (u32 o = 0; o < total; o += 16)
+            *reinterpret_cast<uint4 *>(mine + o) = make_uint4(0u, 0u, 0u, 0u);
+    }
+};
+
+// Whole-region staging for a full wave of small equal-length frames: the wave's
+// 64 slots (64 * stride <= REGION_MAX, stride % 16 == 0) are assembled in LDS
+// and written with contiguous 1 KiB store instructions.  Slot bytes beyond
+// `total` are written as zero.
+struct EmitRegion {
+    static constexpr bool cooperative = true;
+    uint4 *lds;        // 64 * stride bytes
+    uint8_t *wbase;
+    u32 stride, lane, total;
+
+    __device__ __forceinline__ void emit(u32 q, const u32 Din[16])
+    {
+        u32 D[16];
+#pragma unroll
+        for (int k = 0; k < 16; k++)
+            D[k] = Din[k];
+        if (64u * q + 64u > total)
+            mask_chunk(D, total > 64u * q ? total - 64u * q : 0u);
+        const u32 base = (lane * stride + 64u * q) >> 4;
+#pragma unroll
+        for (u32 c = 0; c < 4; c++)
+            if (64u * q + 16u * c < stride)
+                lds[base + c] = make_uint4(D[4 * c], D[4 * c + 1], D[4 * c + 2], D[4 * c + 3]);
+    }
+    __device__ __forceinline__ void tag(const u32 t[4]) { lds[(lane * stride + 16u) >> 4] = make_uint4(t[0], t[1], t[2], t[3]); }
+    __device__ __forceinline__ void finish()
+    {
+        // zero this slot's chunks after the last emitted one
+        const u32 done = ((total + 63u) & ~63u) < stride ? ((total + 63u) & ~63u) : stride;
+        for (u32 o = done; o < stride; o += 16u)
+            lds[(lane * stride + o) >> 4] = make_uint4(0u, 0u, 0u, 0u);
+        const u32 n16 = (64u * stride) >> 4;
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // the other lanes' ds_writes of the region
+        for (u32 k = lane; k < n16; k += 64u)
+            reinterpret_cast<uint4 *>(wbase)[k] = lds[k];
+    }
+    // zero a rejected frame's slot in LDS (per lane), then the converged region store
+    __device__ __forceinline__ void close(bool bad)
+    {
+        if (bad)
+            poison();
+        finish();
+    }
+    __device__ void poison()
+    {
+        for (u32 o = 0; o < stride; o += 16u)
+            lds[(lane * stride + o) >> 4] = make_uint4(0u, 0u, 0u, 0u);
+    }
+};
+
 // --------------------------------------------------------------------------
 // SEAL one frame.
-//   MODE_ZMQ : in = payload (n bytes), out = MESSAGE body (33 + n bytes)
-//   MODE_NACL: in = m (mlen bytes, m[0:32] ignored/zero), out = c (mlen bytes)
+//   MODE_ZMQ : in = payload (n bytes), output = MESSAGE body (33 + n bytes)
+//   MODE_NACL: in = m (n = mlen bytes, m[0:32] ignored), output = c (mlen bytes)
 // key = Salsa20 subkey (HSalsa20 already applied), nonce words from `counter`
 // (ZMQ: BE64 counter; NaCl: the caller passes n[16:24] read big-endian).
 // --------------------------------------------------------------------------
-template <int MODE, bool AL>
-__device__ void seal_frame(const uint8_t *__restrict__ in, uint8_t *__restrict__ out, u32 n, u32 flags, u64 counter,
-                           const u32 key[8])
+template <int MODE, bool AL, class EM>
+__device__ __forceinline__ void seal_frame(const uint8_t *__restrict__ in, u32 n, u32 flags, u64 counter,
+                                           const u32 key[8], EM &em)
 {
-    // Input shift: box byte i comes from in[i - SH] (ZMQ: SH = 33, NaCl: 0).
     // ZMQ funnel: box dword k of block b = alignbyte(P[16b+k-8], P[16b+k-9], 3)
-    // where P[i] is payload dword i; the window of block b is P[16b-8 .. 16b+7]
-    // (payload bytes [64b-32, 64b+32)), and P[16b-9] is carried from block b-1.
+    // where P[i] is payload dword i; block b's window is P[16b-8 .. 16b+7]
+    // (payload bytes [64b-32, 64b+32)) and P[16b-9] is carried from block b-1.
     const u32 mlen = (MODE == MODE_ZMQ) ? n + 33u : n;
     const u32 nfull = mlen >> 6;
     const u32 tailv = mlen & 63u;
-    const u64 inlen = n;  // bytes readable at `in`
+    const u64 inlen = n;
     u32 n0, n1;
     counter_nonce(counter, n0, n1);
 
@@ -157,37 +336,40 @@ __device__ void seal_frame(const uint8_t *__restrict__ in, uint8_t *__restrict__
 
     u32 carry;
     {
-        // block 0: box bytes 32..63
-        u32 W[16];
         if constexpr (MODE == MODE_ZMQ) {
             V4 a = ld16<AL>(in, inlen);
             V4 b = ld16<AL>(in + 16, inlen > 16 ? inlen - 16 : 0);
-            W[7] = flags << 24;  // payload byte -1 is the flag byte (box[32])
-            W[8] = a.x; W[9] = a.y; W[10] = a.z; W[11] = a.w;
-            W[12] = b.x; W[13] = b.y; W[14] = b.z; W[15] = b.w;
+            u32 W[9] = {flags << 24, a.x, a.y, a.z, a.w, b.x, b.y, b.z, b.w};  // P[-1 .. 7]
 #pragma unroll
             for (int k = 8; k < 16; k++)
-                C[k] = funnel(W[k], W[k - 1], 3) ^ x[k];
-            carry = W[15];
+                C[k] = funnel(W[k - 7], W[k - 8], 3) ^ x[k];
+            carry = b.w;
+            C[0] = HDR0; C[1] = HDR1; C[2] = n0; C[3] = n1;
         } else {
             V4 a = ld16<AL>(in + 32, inlen > 32 ? inlen - 32 : 0);
             V4 b = ld16<AL>(in + 48, inlen > 48 ? inlen - 48 : 0);
             C[8] = a.x ^ x[8]; C[9] = a.y ^ x[9]; C[10] = a.z ^ x[10]; C[11] = a.w ^ x[11];
             C[12] = b.x ^ x[12]; C[13] = b.y ^ x[13]; C[14] = b.z ^ x[14]; C[15] = b.w ^ x[15];
             carry = 0;
+            C[0] = C[1] = C[2] = C[3] = 0u;
         }
-        if constexpr (MODE == MODE_ZMQ)
-            st16<AL>(out, HDR0, HDR1, n0, n1);
-        else
-            st16<AL>(out, 0u, 0u, 0u, 0u);
+        C[4] = C[5] = C[6] = C[7] = 0u;  // tag slot, written by em.tag()
         if (nfull >= 1) {
             poly_block(P, C[8], C[9], C[10], C[11], 1u);
             poly_block(P, C[12], C[13], C[14], C[15], 1u);
-            st16<AL>(out + 32, C[8], C[9], C[10], C[11]);
-            st16<AL>(out + 48, C[12], C[13], C[14], C[15]);
         } else {
-            emit_guarded<AL>(P, C, 2, mlen, out, true);
+            if (mlen > 32u) {
+                u32 nb = mlen - 32u;
+                if (nb >= 16u) {
+                    poly_block(P, C[8], C[9], C[10], C[11], 1u);
+                    if (nb > 16u)
+                        poly_block_partial(P, C[12], C[13], C[14], C[15], nb - 16u);
+                } else {
+                    poly_block_partial(P, C[8], C[9], C[10], C[11], nb);
+                }
+            }
         }
+        em.emit(0, C);
     }
 
     // steady state: full 64-byte blocks 1 .. nfull-1, all inputs in range
@@ -220,15 +402,11 @@ __device__ void seal_frame(const uint8_t *__restrict__ in, uint8_t *__restrict__
             for (int k = 0; k < 16; k++)
                 C[k] = W[k] ^ x[k];
         }
-        uint8_t *dst = out + 64u * blk;
-        st16<AL>(dst, C[0], C[1], C[2], C[3]);
-        st16<AL>(dst + 16, C[4], C[5], C[6], C[7]);
-        st16<AL>(dst + 32, C[8], C[9], C[10], C[11]);
-        st16<AL>(dst + 48, C[12], C[13], C[14], C[15]);
         poly_block(P, C[0], C[1], C[2], C[3], 1u);
         poly_block(P, C[4], C[5], C[6], C[7], 1u);
         poly_block(P, C[8], C[9], C[10], C[11], 1u);
         poly_block(P, C[12], C[13], C[14], C[15], 1u);
+        em.emit(blk, C);
     }
 
     // final partial block
@@ -254,58 +432,85 @@ __device__ void seal_frame(const uint8_t *__restrict__ in, uint8_t *__restrict__
             for (int k = 0; k < 16; k++)
                 C[k] = W[k] ^ x[k];
         }
-        emit_guarded<AL>(P, C, 0, tailv, out + 64u * blk, true);
+#pragma unroll
+        for (int j = 0; j < 4; j++) {
+            u32 s = 16u * j;
+            if (s < tailv) {
+                u32 nb = tailv - s;
+                if (nb >= 16)
+                    poly_block(P, C[4 * j], C[4 * j + 1], C[4 * j + 2], C[4 * j + 3], 1u);
+                else
+                    poly_block_partial(P, C[4 * j], C[4 * j + 1], C[4 * j + 2], C[4 * j + 3], nb);
+            }
+        }
+        em.emit(blk, C);
     }
 
     u32 tag[4];
     poly_finish(P, tag);
-    st16<AL>(out + 16, tag[0], tag[1], tag[2], tag[3]);
+    em.tag(tag);
+    em.close(false);
 }
 
 // --------------------------------------------------------------------------
-// OPEN one frame.  Returns a CZ_STATUS_* code.
-//   MODE_ZMQ : in = MESSAGE body (size bytes), out = payload (size - 33 bytes);
+// OPEN one frame.  Returns a CZ_STATUS_* code; the emitter receives the output:
+//   MODE_ZMQ : in = MESSAGE body (size bytes), output = payload (size - 33 bytes);
 //              *flags_out = box[32]; *nonce_out = BE64(body[8:16]).
-//   MODE_NACL: in = c (size bytes), out = m (size bytes, m[0:32] = 0).
+//   MODE_NACL: in = c (size bytes), output = m (size bytes, m[0:32] = 0).
 // The replay check of decode (CurveClientMechanism.java:186-193) compares the
 // frame nonce against `floor` as signed 64-bit values, like Java's long.
-// On a bad tag the plaintext already written is overwritten with zeros.
+// On a bad tag the emitted plaintext is overwritten with zeros (em.poison()).
+// Frames rejected before decryption emit nothing.
 // --------------------------------------------------------------------------
-template <int MODE, bool AL>
-__device__ u32 open_frame(const uint8_t *__restrict__ in, uint8_t *__restrict__ out, u32 size, const u32 key_in[8],
-                          bool check_floor, long long floor, u32 *flags_out, u64 *nonce_out, u64 nacl_counter)
+template <int MODE, bool AL, class EM>
+__device__ __forceinline__ u32 open_frame(const uint8_t *__restrict__ in, u32 size, const u32 key[8],
+                                          bool check_floor, long long floor, u32 *flags_out, u64 *nonce_out,
+                                          u64 nacl_counter, EM &em)
 {
+    // A cooperative emitter needs every lane of the wave in the same chunk
+    // sequence: a frame rejected before decryption then runs through the
+    // (uniform-size) loop as a dead lane that emits zeros.
+    constexpr bool COOP = EM::cooperative;
+    u32 early = CZ_STATUS_OK;
     u32 n0, n1;
     if constexpr (MODE == MODE_ZMQ) {
         // Msgs.startsWith(msg, "MESSAGE", true) (zmq/io/Msgs.java:20-39): size >= 8,
         // byte 0 == 7, bytes 1..6 == "MESSAG" (its loop never reaches byte 7).
-        if (size < 8u)
-            return CZ_STATUS_COMMAND;
         V4 h = ld16<AL>(in, size);
-        if (h.x != HDR0 || (h.y & 0x00ffffffu) != (HDR1 & 0x00ffffffu))
-            return CZ_STATUS_COMMAND;
-        if (size < 33u)
-            return CZ_STATUS_MALFORMED;
+        if (size < 8u || h.x != HDR0 || (h.y & 0x00ffffffu) != (HDR1 & 0x00ffffffu))
+            early = CZ_STATUS_COMMAND;
+        else if (size < 33u)
+            early = CZ_STATUS_MALFORMED;
         n0 = h.z;
         n1 = h.w;
-        u64 nonce = ((u64)bswap32(n0) << 32) | (u64)bswap32(n1);
-        *nonce_out = nonce;
-        if (check_floor && (long long)nonce <= floor)
-            return CZ_STATUS_SEQUENCE;
+        if (early == CZ_STATUS_OK) {
+            u64 nonce = ((u64)bswap32(n0) << 32) | (u64)bswap32(n1);
+            *nonce_out = nonce;
+            if (check_floor && (long long)nonce <= floor)
+                early = CZ_STATUS_SEQUENCE;
+        }
     } else {
         if (size < 32u)
-            return CZ_STATUS_MALFORMED;
+            early = CZ_STATUS_MALFORMED;
         counter_nonce(nacl_counter, n0, n1);
     }
-    u32 key[8];
-#pragma unroll
-    for (int i = 0; i < 8; i++)
-        key[i] = key_in[i];
+    if (early != CZ_STATUS_OK && (!COOP || size < 33u))
+        return early;  // cooperative callers only launch uniform sizes >= 33
+    const bool dead = early != CZ_STATUS_OK;
 
     const u32 mlen = size;
+    const u32 nblk = (mlen + 63u) >> 6;
     const u32 nfull = mlen >> 6;
-    const u32 tailv = mlen & 63u;
-    const u32 nout = (MODE == MODE_ZMQ) ? size - 33u : size;  // bytes writable at out
+    const u32 nout = (MODE == MODE_ZMQ) ? size - 33u : size;
+
+    auto emit_open = [&](u32 q, u32 D[16]) {
+        if (COOP && dead) {
+#pragma unroll
+            for (int k = 0; k < 16; k++)
+                D[k] = 0u;
+        }
+        em.emit(q, D);
+    };
 
     u32 x[16], C[16], X[16];
     salsa20_block(x, key, n0, n1, 0u, 0u);
@@ -313,36 +518,10 @@ __device__ u32 open_frame(const uint8_t *__restrict__ in, uint8_t *__restrict__ 
     poly_init(P, x[0], x[1], x[2], x[3], x[4], x[5], x[6], x[7]);
     V4 tin = ld16<AL>(in + 16, size - 16u);
 
-    // ZMQ output schedule: payload dword j = alignbyte(D[j+9], D[j+8], 1) with D the
-    // plaintext box dwords.  After block b the lane emits payload bytes
-    // [64b-48, 64b+16) from D[16b-4 .. 16b+12]; D[16b-4 .. 16b-1] is the carry.
-    u32 cy0 = 0, cy1 = 0, cy2 = 0, cy3 = 0;
-
-    auto emit_zmq = [&](u32 blk, const u32 D[16], bool guarded) {
-        // E[i] = D[16b-4+i], i = 0..16  (E[0..3] = carry, E[4..19] = D)
-        u32 E[20] = {cy0, cy1, cy2, cy3, D[0], D[1], D[2], D[3], D[4], D[5], D[6], D[7],
-                     D[8], D[9], D[10], D[11], D[12], D[13], D[14], D[15]};
-        long base = (long)(64u * blk) - 48;  // payload byte offset of the first emitted chunk
-#pragma unroll
-        for (int c = 0; c < 4; c++) {
-            // payload dword j = 16b-12 + 4c + t  ->  D[j+8] = E[4c+t], D[j+9] = E[4c+t+1]
-            u32 o0 = funnel(E[4 * c + 1], E[4 * c + 0], 1);
-            u32 o1 = funnel(E[4 * c + 2], E[4 * c + 1], 1);
-            u32 o2 = funnel(E[4 * c + 3], E[4 * c + 2], 1);
-            u32 o3 = funnel(E[4 * c + 4], E[4 * c + 3], 1);
-            long o = base + 16 * c;
-            if (!guarded) {
-                st16<AL>(out + o, o0, o1, o2, o3);
-            } else if (o >= 0 && (u64)o < nout) {
-                u64 rem = nout - (u64)o;
-                if (rem >= 16)
-                    st16<AL>(out + o, o0, o1, o2, o3);
-                else
-                    st_bytes(out + o, o0, o1, o2, o3, (u32)rem);
-            }
-        }
-        cy0 = D[12]; cy1 = D[13]; cy2 = D[14]; cy3 = D[15];
-    };
+    // ZMQ: payload chunk m (bytes [64m, 64m+64)) = box [64m+33, 64m+97): dword t is
+    // alignbyte(D[16m+t+9], D[16m+t+8], 1), D = plaintext box dwords.  It is emitted
+    // after block m+1, from block m's dwords 8..15 (the carry) and block m+1's 0..8.
+    u32 K[8];
 
     // block 0
     {
@@ -350,127 +529,112 @@ __device__ u32 open_frame(const uint8_t *__restrict__ in, uint8_t *__restrict__ 
         V4 b = ld16<AL>(in + 48, size > 48 ? size - 48u : 0);
         C[8] = a.x; C[9] = a.y; C[10] = a.z; C[11] = a.w;
         C[12] = b.x; C[13] = b.y; C[14] = b.z; C[15] = b.w;
-#pragma unroll
-        for (int k = 0; k < 8; k++)
-            C[k] = 0;
         if (nfull >= 1) {
             poly_block(P, C[8], C[9], C[10], C[11], 1u);
             poly_block(P, C[12], C[13], C[14], C[15], 1u);
-        } else {
-            emit_guarded<AL>(P, C, 2, mlen, nullptr, false);
+        } else if (mlen > 32u) {
+            u32 nb = mlen - 32u;
+            if (nb >= 16u) {
+                poly_block(P, C[8], C[9], C[10], C[11], 1u);
+                if (nb > 16u)
+                    poly_block_partial(P, C[12], C[13], C[14], C[15], nb - 16u);
+            } else {
+                poly_block_partial(P, C[8], C[9], C[10], C[11], nb);
+            }
         }
 #pragma unroll
-        for (int k = 0; k < 16; k++)
-            X[k] = k < 8 ? 0u : (C[k] ^ x[k]);
+        for (int k = 8; k < 16; k++)
+            X[k] = C[k] ^ x[k];
         if constexpr (MODE == MODE_ZMQ) {
             *flags_out = X[8] & 0xffu;
-            emit_zmq(0, X, true);
-        } else {
-            if (nfull >= 1) {
-                st16<AL>(out, 0u, 0u, 0u, 0u);
-                st16<AL>(out + 16, 0u, 0u, 0u, 0u);
-                st16<AL>(out + 32, X[8], X[9], X[10], X[11]);
-                st16<AL>(out + 48, X[12], X[13], X[14], X[15]);
-            } else {
 #pragma unroll
-                for (int c = 0; c < 4; c++) {
-                    u32 s = 16u * c;
-                    if (s < mlen) {
-                        u32 nb = mlen - s;
-                        if (nb >= 16)
-                            st16<AL>(out + s, X[4 * c], X[4 * c + 1], X[4 * c + 2], X[4 * c + 3]);
-                        else
-                            st_bytes(out + s, X[4 * c], X[4 * c + 1], X[4 * c + 2], X[4 * c + 3], nb);
-                    }
-                }
-            }
+            for (int k = 0; k < 8; k++)
+                K[k] = X[8 + k];
+        } else {
+#pragma unroll
+            for (int k = 0; k < 8; k++)
+                X[k] = 0u;
+            emit_open(0, X);
         }
     }
 
-    for (u32 blk = 1; blk < nfull; blk++) {
+    for (u32 blk = 1; blk < nblk; blk++) {
         const uint8_t *src = in + 64u * blk;
-        V4 q0 = ld16f<AL>(src), q1 = ld16f<AL>(src + 16), q2 = ld16f<AL>(src + 32), q3 = ld16f<AL>(src + 48);
+        V4 q0, q1, q2, q3;
+        const bool full = blk < nfull;
+        if (full) {
+            q0 = ld16f<AL>(src);
+            q1 = ld16f<AL>(src + 16);
+            q2 = ld16f<AL>(src + 32);
+            q3 = ld16f<AL>(src + 48);
+        } else {
+            const u32 o = 64u * blk;
+            q0 = ld16<AL>(src, size - o);
+            q1 = ld16<AL>(src + 16, o + 16u < size ? size - o - 16u : 0);
+            q2 = ld16<AL>(src + 32, o + 32u < size ? size - o - 32u : 0);
+            q3 = ld16<AL>(src + 48, o + 48u < size ? size - o - 48u : 0);
+        }
         salsa20_block(x, key, n0, n1, blk, 0u);
         C[0] = q0.x; C[1] = q0.y; C[2] = q0.z; C[3] = q0.w;
         C[4] = q1.x; C[5] = q1.y; C[6] = q1.z; C[7] = q1.w;
         C[8] = q2.x; C[9] = q2.y; C[10] = q2.z; C[11] = q2.w;
         C[12] = q3.x; C[13] = q3.y; C[14] = q3.z; C[15] = q3.w;
-        poly_block(P, C[0], C[1], C[2], C[3], 1u);
-        poly_block(P, C[4], C[5], C[6], C[7], 1u);
-        poly_block(P, C[8], C[9], C[10], C[11], 1u);
-        poly_block(P, C[12], C[13], C[14], C[15], 1u);
+        if (full) {
+            poly_block(P, C[0], C[1], C[2], C[3], 1u);
+            poly_block(P, C[4], C[5], C[6], C[7], 1u);
+            poly_block(P, C[8], C[9], C[10], C[11], 1u);
+            poly_block(P, C[12], C[13], C[14], C[15], 1u);
+        } else {
+            const u32 tailv = mlen - 64u * blk;
+#pragma unroll
+            for (int j = 0; j < 4; j++) {
+                u32 s = 16u * j;
+                if (s < tailv) {
+                    u32 nb = tailv - s;
+                    if (nb >= 16)
+                        poly_block(P, C[4 * j], C[4 * j + 1], C[4 * j + 2], C[4 * j + 3], 1u);
+                    else
+                        poly_block_partial(P, C[4 * j], C[4 * j + 1], C[4 * j + 2], C[4 * j + 3], nb);
+                }
+            }
+        }
 #pragma unroll
         for (int k = 0; k < 16; k++)
             X[k] = C[k] ^ x[k];
         if constexpr (MODE == MODE_ZMQ) {
-            emit_zmq(blk, X, false);
+            u32 O[16];
+            u32 E[17] = {K[0], K[1], K[2], K[3], K[4], K[5], K[6], K[7], X[0], X[1], X[2], X[3], X[4], X[5], X[6],
+                         X[7], X[8]};
+#pragma unroll
+            for (int t = 0; t < 16; t++)
+                O[t] = funnel(E[t + 1], E[t], 1);
+            emit_open(blk - 1, O);
+#pragma unroll
+            for (int k = 0; k < 8; k++)
+                K[k] = X[8 + k];
         } else {
-            uint8_t *dst = out + 64u * blk;
-            st16<AL>(dst, X[0], X[1], X[2], X[3]);
-            st16<AL>(dst + 16, X[4], X[5], X[6], X[7]);
-            st16<AL>(dst + 32, X[8], X[9], X[10], X[11]);
-            st16<AL>(dst + 48, X[12], X[13], X[14], X[15]);
+            emit_open(blk, X);
         }
-    }
-
-    u32 total_blocks = nfull;
-    if (tailv != 0 && nfull >= 1) {
-        const u32 blk = nfull;
-        const uint8_t *src = in + 64u * blk;
-        V4 q[4];
-#pragma unroll
-        for (int c = 0; c < 4; c++) {
-            u32 o = 64u * blk + 16u * c;
-            q[c] = ld16<AL>(src + 16 * c, o < size ? size - o : 0);
-        }
-        salsa20_block(x, key, n0, n1, blk, 0u);
-        u32 Q[16] = {q[0].x, q[0].y, q[0].z, q[0].w, q[1].x, q[1].y, q[1].z, q[1].w,
-                     q[2].x, q[2].y, q[2].z, q[2].w, q[3].x, q[3].y, q[3].z, q[3].w};
-        emit_guarded<AL>(P, Q, 0, tailv, nullptr, false);
-#pragma unroll
-        for (int k = 0; k < 16; k++)
-            X[k] = Q[k] ^ x[k];
-        if constexpr (MODE == MODE_ZMQ) {
-            emit_zmq(blk, X, true);
-        } else {
-            uint8_t *dst = out + 64u * blk;
-#pragma unroll
-            for (int c = 0; c < 4; c++) {
-                u32 s = 16u * c;
-                if (s < tailv) {
-                    u32 nb = tailv - s;
-                    if (nb >= 16)
-                        st16<AL>(dst + s, X[4 * c], X[4 * c + 1], X[4 * c + 2], X[4 * c + 3]);
-                    else
-                        st_bytes(dst + s, X[4 * c], X[4 * c + 1], X[4 * c + 2], X[4 * c + 3], nb);
-                }
-            }
-        }
-        total_blocks = nfull + 1;
-    } else if (nfull == 0) {
-        total_blocks = 1;
     }
     if constexpr (MODE == MODE_ZMQ) {
-        // flush: payload bytes [64B-48, 64B+16) from the carry (D beyond the box are zero)
-        u32 Z[16] = {0u, 0u, 0u, 0u, 0u, 0u, 0u, 0u, 0u, 0u, 0u, 0u, 0u, 0u, 0u, 0u};
-        emit_zmq(total_blocks, Z, true);
+        // last payload chunk nblk-1 (if any payload remains): block nblk is beyond the box
+        if (64u * (nblk - 1u) < nout) {
+            u32 O[16];
+#pragma unroll
+            for (int t = 0; t < 16; t++)
+                O[t] = t < 7 ? funnel(K[t + 1], K[t], 1) : (t == 7 ? funnel(0u, K[7], 1) : 0u);
+            emit_open(nblk - 1u, O);
+        }
     }
 
     u32 tag[4];
     poly_finish(P, tag);
     u32 diff = (tag[0] ^ tin.x) | (tag[1] ^ tin.y) | (tag[2] ^ tin.z) | (tag[3] ^ tin.w);
-    if (diff != 0) {
-        // never release unauthenticated plaintext
-        for (u32 o = 0; o < nout; o += 16) {
-            u32 nb = nout - o < 16 ? nout - o : 16;
-            if (nb == 16)
-                st16<AL>(out + o, 0u, 0u, 0u, 0u);
-            else
-                st_bytes(out + o, 0u, 0u, 0u, 0u, nb);
-        }
-        return CZ_STATUS_CRYPTO;
-    }
-    return CZ_STATUS_OK;
+    const bool bad = dead || diff != 0;
+    em.close(bad);  // never release unauthenticated plaintext; converged for cooperative emitters
+    if (dead)
+        return early;
+    return diff != 0 ? (u32)CZ_STATUS_CRYPTO : (u32)CZ_STATUS_OK;
 }
 
 __device__ __forceinline__ void load_key(const uint8_t *__restrict__ p, u32 k[8])
@@ -486,30 +650,65 @@ __device__ __forceinline__ bool aligned16(const void *a, const void *b)
     return (((uintptr_t)a | (uintptr_t)b) & 15u) == 0;
 }
 
+__device__ __forceinline__ u64 read_be64(const uint8_t *p)
+{
+    u64 v = 0;
+    for (int b = 0; b < 8; b++)
+        v = (v << 8) | p[b];
+    return v;
+}
+
 // ---- kernels -------------------------------------------------------------
 
-constexpr int BLOCK = 256;
+enum Staging { ST_DIRECT = 0, ST_LINES = 1, ST_REGION = 2 };
 
-// Uniform batch: frame i = in[i*in_stride .. +len) -> out[i*out_stride .. +len+33),
-// nonce counter = counter0 + i, flags = flags8 ? flags8[i] : 0, one subkey.
+// Uniform batch of one connection direction: frame i = in[i*in_stride .. +len)
+// -> slot out[i*out_stride .. +out_stride), nonce counter0 + i, flags8[i] (or 0).
+// ST_LINES / ST_REGION need the launcher's preconditions (see czk_seal_uniform);
+// a wave with fewer than 64 frames always stores directly.
+template <int ST>
 __global__ __launch_bounds__(BLOCK) void k_seal_uniform(const uint8_t *__restrict__ in, uint64_t in_stride,
                                                          uint8_t *__restrict__ out, uint64_t out_stride,
                                                          uint32_t count, uint32_t len,
                                                          const uint8_t *__restrict__ subkey, uint64_t counter0,
                                                          const uint8_t *__restrict__ flags8)
 {
+    extern __shared__ uint4 smem[];
     const uint32_t i = blockIdx.x * BLOCK + threadIdx.x;
-    if (i >= count)
+    const uint32_t wave_first = i & ~63u;
+    if (wave_first >= count)
         return;
     u32 key[8];
     load_key(subkey, key);
+    const bool full_wave = wave_first + 64u <= count;
     const uint8_t *src = in + (uint64_t)i * in_stride;
     uint8_t *dst = out + (uint64_t)i * out_stride;
+    const u32 mlen = len + 33u;
+    if (ST != ST_DIRECT && full_wave) {
+        const u32 fl = flags8 ? flags8[i] : 0u;
+        const u32 lane = threadIdx.x & 63u;
+        if constexpr (ST == ST_LINES) {
+            EmitLines em{smem + (threadIdx.x >> 6) * (LINE_LDS_BYTES / 16), out + (uint64_t)wave_first * out_stride,
+                         dst, out_stride, lane, mlen, 0u, true};
+            seal_frame<MODE_ZMQ, true>(src, len, fl, counter0 + i, key, em);
+        } else {
+            const u32 st = (u32)out_stride;
+            EmitRegion em{smem + (threadIdx.x >> 6) * ((64u * st) >> 4), out + (uint64_t)wave_first * out_stride, st,
+                          lane, mlen};
+            seal_frame<MODE_ZMQ, true>(src, len, fl, counter0 + i, key, em);
+        }
+        return;
+    }
+    if (i >= count)
+        return;
     const u32 fl = flags8 ? flags8[i] : 0u;
-    if (aligned16(src, dst))
-        seal_frame<MODE_ZMQ, true>(src, dst, len, fl, counter0 + i, key);
-    else
-        seal_frame<MODE_ZMQ, false>(src, dst, len, fl, counter0 + i, key);
+    if (aligned16(src, dst)) {
+        EmitDirect<true> em{dst, mlen};
+        seal_frame<MODE_ZMQ, true>(src, len, fl, counter0 + i, key, em);
+    } else {
+        EmitDirect<false> em{dst, mlen};
+        seal_frame<MODE_ZMQ, false>(src, len, fl, counter0 + i, key, em);
+    }
 }
 
 __global__ __launch_bounds__(BLOCK) void k_seal_desc(const cz_frame_desc *__restrict__ desc,
@@ -526,10 +725,13 @@ __global__ __launch_bounds__(BLOCK) void k_seal_desc(const cz_frame_desc *__rest
     load_key(subkeys + 32ull * d.key_idx, key);
     const uint8_t *src = in + d.in_off;
     uint8_t *dst = out + d.out_off;
-    if (aligned16(src, dst))
-        seal_frame<MODE_ZMQ, true>(src, dst, d.len, d.flags & 0xffu, d.counter, key);
-    else
-        seal_frame<MODE_ZMQ, false>(src, dst, d.len, d.flags & 0xffu, d.counter, key);
+    if (aligned16(src, dst)) {
+        EmitDirect<true> em{dst, d.len + 33u};
+        seal_frame<MODE_ZMQ, true>(src, d.len, d.flags & 0xffu, d.counter, key, em);
+    } else {
+        EmitDirect<false> em{dst, d.len + 33u};
+        seal_frame<MODE_ZMQ, false>(src, d.len, d.flags & 0xffu, d.counter, key, em);
+    }
 }
 
 // status[i] = CZ_STATUS_* | (flags byte << 8)
@@ -550,11 +752,7 @@ __global__ __launch_bounds__(BLOCK) void k_open_desc(const cz_frame_desc *__rest
     if (d.prev >= 0) {
         // replay floor = nonce of the previous frame of this connection in the batch
         const cz_frame_desc p = desc[d.prev];
-        const uint8_t *pb = in + p.in_off + 8;
-        u64 v = 0;
-        for (int b = 0; b < 8; b++)
-            v = (v << 8) | pb[b];
-        floor = (long long)v;
+        floor = (long long)read_be64(in + p.in_off + 8);
     }
     const bool check = (d.flags & CZ_DESC_CHECK_NONCE) != 0;
     const uint8_t *src = in + d.in_off;
@@ -562,44 +760,69 @@ __global__ __launch_bounds__(BLOCK) void k_open_desc(const cz_frame_desc *__rest
     u32 fl = 0;
     u64 nonce = 0;
     u32 st;
-    if (aligned16(src, dst))
-        st = open_frame<MODE_ZMQ, true>(src, dst, d.len, key, check, floor, &fl, &nonce, 0);
-    else
-        st = open_frame<MODE_ZMQ, false>(src, dst, d.len, key, check, floor, &fl, &nonce, 0);
+    const u32 nout = d.len >= 33u ? d.len - 33u : 0u;
+    if (aligned16(src, dst)) {
+        EmitDirect<true> em{dst, nout};
+        st = open_frame<MODE_ZMQ, true>(src, d.len, key, check, floor, &fl, &nonce, 0, em);
+    } else {
+        EmitDirect<false> em{dst, nout};
+        st = open_frame<MODE_ZMQ, false>(src, d.len, key, check, floor, &fl, &nonce, 0, em);
+    }
     status[i] = (uint16_t)(st | (st == CZ_STATUS_OK ? (fl << 8) : 0u));
     if (nonces)
         nonces[i] = nonce;
 }
 
+// Uniform open of one connection's bodies in order: frame i must beat frame
+// i-1's nonce, frame 0 must beat floor0 (when check != 0).
+template <int ST>
 __global__ __launch_bounds__(BLOCK) void k_open_uniform(const uint8_t *__restrict__ in, uint64_t in_stride,
                                                          uint8_t *__restrict__ out, uint64_t out_stride,
                                                          uint32_t count, uint32_t size,
                                                          const uint8_t *__restrict__ subkey, uint64_t floor0,
                                                          int check, uint16_t *__restrict__ status)
 {
+    extern __shared__ uint4 smem[];
     const uint32_t i = blockIdx.x * BLOCK + threadIdx.x;
-    if (i >= count)
+    const uint32_t wave_first = i & ~63u;
+    if (wave_first >= count)
         return;
     u32 key[8];
     load_key(subkey, key);
+    const bool full_wave = wave_first + 64u <= count;
     const uint8_t *src = in + (uint64_t)i * in_stride;
     uint8_t *dst = out + (uint64_t)i * out_stride;
-    // frames of one connection in order: frame i must beat frame i-1's nonce
-    long long floor = (long long)floor0;
-    if (i > 0) {
-        const uint8_t *pb = src - in_stride + 8;
-        u64 v = 0;
-        for (int b = 0; b < 8; b++)
-            v = (v << 8) | pb[b];
-        floor = (long long)v;
-    }
+    const u32 nout = size >= 33u ? size - 33u : 0u;
     u32 fl = 0;
     u64 nonce = 0;
     u32 st;
-    if (aligned16(src, dst))
-        st = open_frame<MODE_ZMQ, true>(src, dst, size, key, check != 0, floor, &fl, &nonce, 0);
-    else
-        st = open_frame<MODE_ZMQ, false>(src, dst, size, key, check != 0, floor, &fl, &nonce, 0);
+    if (ST != ST_DIRECT && full_wave) {
+        long long floor = i > 0 ? (long long)read_be64(src - in_stride + 8) : (long long)floor0;
+        const u32 lane = threadIdx.x & 63u;
+        if constexpr (ST == ST_LINES) {
+            EmitLines em{smem + (threadIdx.x >> 6) * (LINE_LDS_BYTES / 16), out + (uint64_t)wave_first * out_stride,
+                         dst, out_stride, lane, nout, 0u, false};
+            st = open_frame<MODE_ZMQ, true>(src, size, key, check != 0, floor, &fl, &nonce, 0, em);
+        } else {
+            const u32 ost = (u32)out_stride;
+            EmitRegion em{smem + (threadIdx.x >> 6) * ((64u * ost) >> 4), out + (uint64_t)wave_first * out_stride,
+                          ost, lane, nout};
+            st = open_frame<MODE_ZMQ, true>(src, size, key, check != 0, floor, &fl, &nonce, 0, em);
+        }
+        // rejected frames ran the loop as dead lanes: their slots hold zeros
+        status[i] = (uint16_t)(st | (st == CZ_STATUS_OK ? (fl << 8) : 0u));
+        return;
+    }
+    if (i >= count)
+        return;
+    long long floor = i > 0 ? (long long)read_be64(src - in_stride + 8) : (long long)floor0;
+    if (aligned16(src, dst)) {
+        EmitDirect<true> em{dst, nout};
+        st = open_frame<MODE_ZMQ, true>(src, size, key, check != 0, floor, &fl, &nonce, 0, em);
+    } else {
+        EmitDirect<false> em{dst, nout};
+        st = open_frame<MODE_ZMQ, false>(src, size, key, check != 0, floor, &fl, &nonce, 0, em);
+    }
     status[i] = (uint16_t)(st | (st == CZ_STATUS_OK ? (fl << 8) : 0u));
 }
 
@@ -618,19 +841,25 @@ __global__ __launch_bounds__(64) void k_box_nacl(const uint8_t *__restrict__ in,
             *rc = -1;
             return;
         }
-        if (aligned16(in, out))
-            seal_frame<MODE_NACL, true>(in, out, len, 0u, counter, key);
-        else
-            seal_frame<MODE_NACL, false>(in, out, len, 0u, counter, key);
+        if (aligned16(in, out)) {
+            EmitDirect<true> em{out, len};
+            seal_frame<MODE_NACL, true>(in, len, 0u, counter, key, em);
+        } else {
+            EmitDirect<false> em{out, len};
+            seal_frame<MODE_NACL, false>(in, len, 0u, counter, key, em);
+        }
         *rc = 0;
     } else {
         u32 fl;
         u64 nonce;
         u32 st;
-        if (aligned16(in, out))
-            st = open_frame<MODE_NACL, true>(in, out, len, key, false, 0, &fl, &nonce, counter);
-        else
-            st = open_frame<MODE_NACL, false>(in, out, len, key, false, 0, &fl, &nonce, counter);
+        if (aligned16(in, out)) {
+            EmitDirect<true> em{out, len};
+            st = open_frame<MODE_NACL, true>(in, len, key, false, 0, &fl, &nonce, counter, em);
+        } else {
+            EmitDirect<false> em{out, len};
+            st = open_frame<MODE_NACL, false>(in, len, key, false, 0, &fl, &nonce, counter, em);
+        }
         *rc = st == CZ_STATUS_OK ? 0 : -1;
     }
 }
@@ -678,7 +907,18 @@ __global__ __launch_bounds__(BLOCK) void k_fill(uint8_t *__restrict__ buf, uint6
     }
 }
 
-// Lay out uniform-length frames into a packed strided layout (tests / host staging).
+// Staging choice for a uniform batch (all pointers 16-byte aligned assumed by the caller check).
+int pick_staging(uint64_t stride, uint32_t out_bytes, bool aligned)
+{
+    if (!aligned)
+        return ST_DIRECT;
+    if (stride % 128 == 0 && out_bytes >= 256 && stride <= 0xffffffffull)
+        return ST_LINES;
+    if (stride % 16 == 0 && 64 * stride <= REGION_MAX)
+        return ST_REGION;
+    return ST_DIRECT;
+}
+
 }  // namespace
 
 // ---------------------------------------------------------------------------
@@ -694,8 +934,22 @@ hipError_t czk_seal_uniform(const void *in, uint64_t in_stride, void *out, uint6
     if (count == 0)
         return hipSuccess;
     dim3 grid((count + BLOCK - 1) / BLOCK);
-    hipLaunchKernelGGL(k_seal_uniform, grid, dim3(BLOCK), 0, s, (const uint8_t *)in, in_stride, (uint8_t *)out,
-                       out_stride, count, len, (const uint8_t *)subkey, counter0, flags8);
+    const bool al = ((((uintptr_t)in | (uintptr_t)out | in_stride | out_stride) & 15u) == 0);
+    switch (pick_staging(out_stride, len + 33u, al)) {
+    case ST_LINES:
+        hipLaunchKernelGGL(k_seal_uniform<ST_LINES>, grid, dim3(BLOCK), WAVES * LINE_LDS_BYTES, s,
+                           (const uint8_t *)in, in_stride, (uint8_t *)out, out_stride, count, len,
+                           (const uint8_t *)subkey, counter0, flags8);
+        break;
+    case ST_REGION:
+        hipLaunchKernelGGL(k_seal_uniform<ST_REGION>, grid, dim3(BLOCK), (unsigned)(WAVES * 64 * out_stride), s,
+                           (const uint8_t *)in, in_stride, (uint8_t *)out, out_stride, count, len,
+                           (const uint8_t *)subkey, counter0, flags8);
+        break;
+    default:
+        hipLaunchKernelGGL(k_seal_uniform<ST_DIRECT>, grid, dim3(BLOCK), 0, s, (const uint8_t *)in, in_stride,
+                           (uint8_t *)out, out_stride, count, len, (const uint8_t *)subkey, counter0, flags8);
+    }
     return hipGetLastError();
 }
 
@@ -728,8 +982,23 @@ hipError_t czk_open_uniform(const void *in, uint64_t in_stride, void *out, uint6
     if (count == 0)
         return hipSuccess;
     dim3 grid((count + BLOCK - 1) / BLOCK);
-    hipLaunchKernelGGL(k_open_uniform, grid, dim3(BLOCK), 0, s, (const uint8_t *)in, in_stride, (uint8_t *)out,
-                       out_stride, count, size, (const uint8_t *)subkey, floor0, check, status);
+    const bool al = ((((uintptr_t)in | (uintptr_t)out | in_stride | out_stride) & 15u) == 0);
+    const uint32_t nout = size >= 33u ? size - 33u : 0u;
+    switch (size >= 33u ? pick_staging(out_stride, nout, al) : ST_DIRECT) {
+    case ST_LINES:
+        hipLaunchKernelGGL(k_open_uniform<ST_LINES>, grid, dim3(BLOCK), WAVES * LINE_LDS_BYTES, s,
+                           (const uint8_t *)in, in_stride, (uint8_t *)out, out_stride, count, size,
+                           (const uint8_t *)subkey, floor0, check, status);
+        break;
+    case ST_REGION:
+        hipLaunchKernelGGL(k_open_uniform<ST_REGION>, grid, dim3(BLOCK), (unsigned)(WAVES * 64 * out_stride), s,
+                           (const uint8_t *)in, in_stride, (uint8_t *)out, out_stride, count, size,
+                           (const uint8_t *)subkey, floor0, check, status);
+        break;
+    default:
+        hipLaunchKernelGGL(k_open_uniform<ST_DIRECT>, grid, dim3(BLOCK), 0, s, (const uint8_t *)in, in_stride,
+                           (uint8_t *)out, out_stride, count, size, (const uint8_t *)subkey, floor0, check, status);
+    }
     return hipGetLastError();
 }
 

@@ -234,40 +234,100 @@ def test_ragged_zipf_vs_oracle(torch_dev, subkeys):
     assert np.array_equal(out, want)
 
 
-def test_uniform_4k_vs_oracle_and_roundtrip(torch_dev, subkeys, L):
+def _oracle_uniform(hin, in_stride, count, n, flags, counter0):
+    desc = np.zeros(count, dtype=DESC_DTYPE)
+    desc["in_off"] = np.arange(count, dtype=np.uint64) * in_stride
+    desc["out_off"] = np.arange(count, dtype=np.uint64) * (n + 33)
+    desc["len"] = n
+    desc["counter"] = counter0 + np.arange(count, dtype=np.uint64)
+    desc["flags"] = flags
+    return _oracle_seal(desc, hin, count * (n + 33)).reshape(count, n + 33)
+
+
+# (payload length, in_stride, out_stride, count): exercises every output stager --
+# LINES (out_stride % 128 == 0), REGION (64 slots <= 16 KiB), DIRECT -- and partial waves
+UNIFORM_CASES = [
+    (4096, 4096, 4224, 4096),        # LINES, the benchmark layout
+    (4096, 4096, 4224, 4096 + 37),   # LINES + a partial last wave (direct)
+    (4096, 4096, 4144, 1000),        # DIRECT (stride not a line multiple)
+    (100, 112, 144, 4096 + 5),       # REGION, the 100 B benchmark layout
+    (100, 112, 256, 640),            # REGION with 256-byte slots
+    (1000, 1008, 1152, 777),         # LINES, mid-size
+    (223, 224, 256, 300),            # body 256 B exactly: LINES
+    (0, 16, 48, 200),                # empty payloads: REGION
+    (31, 32, 128, 130),              # body = 64 B (block-0 only): REGION
+]
+
+
+@pytest.mark.parametrize("n,in_stride,out_stride,count", UNIFORM_CASES)
+def test_uniform_seal_open_vs_oracle(torch_dev, subkeys, n, in_stride, out_stride, count):
     torch, dev = torch_dev
     from jeromq_amd import batch
-    count, n = 4096, 4096
-    in_stride, out_stride = 4096, 4144
-    d_in = torch.empty(count * in_stride, dtype=torch.uint8, device=dev)
-    batch.fill(d_in, 0x5EED0002)
+    d_in = torch.empty(max(count * in_stride, 16), dtype=torch.uint8, device=dev)
+    batch.fill(d_in, 0x5EED0002 + n)
     flags = torch.zeros(count, dtype=torch.uint8, device=dev)
     flags[::8] = 1
-    d_out = torch.zeros(count * out_stride, dtype=torch.uint8, device=dev)
+    flags[3::8] = 2
+    d_out = torch.full((count * out_stride,), 0xAB, dtype=torch.uint8, device=dev)
     batch.seal_uniform(d_in, in_stride, d_out, out_stride, count, n, subkeys[0], 3, flags8=flags)
     torch.cuda.synchronize()
     hin = d_in.cpu().numpy()
-    assert hin[:64].tobytes() == splitmix_words(8, 0x5EED0002).view(np.uint8).tobytes()
-    desc = np.zeros(count, dtype=DESC_DTYPE)
-    desc["in_off"] = np.arange(count, dtype=np.uint64) * in_stride
-    desc["out_off"] = np.arange(count, dtype=np.uint64) * out_stride
-    desc["len"] = n
-    desc["counter"] = 3 + np.arange(count, dtype=np.uint64)
-    desc["flags"] = flags.cpu().numpy()
-    want = _oracle_seal(desc, hin, count * out_stride)
-    got = d_out.cpu().numpy()
-    for i in range(count):
-        o = i * out_stride
-        assert got[o:o + n + 33].tobytes() == want[o:o + n + 33].tobytes(), f"frame {i}"
-    # open back, in order, replay-checked
-    d_plain = torch.zeros(count * in_stride, dtype=torch.uint8, device=dev)
+    fl = flags.cpu().numpy()
+    want = _oracle_uniform(hin, in_stride, count, n, fl, 3)
+    got = d_out.cpu().numpy().reshape(count, out_stride)
+    bad = np.nonzero(np.any(got[:, :n + 33] != want, axis=1))[0]
+    assert len(bad) == 0, f"{len(bad)} frames differ, first {bad[:5]}"
+    # slot padding: written as zero by the staged paths, untouched (0xAB) by the direct path
+    pad = got[:, n + 33:]
+    assert np.all((pad == 0) | (pad == 0xAB))
+    # open back, in order, replay-checked, into payload slots of in_stride bytes
+    d_plain = torch.full((count * in_stride,), 0xCD, dtype=torch.uint8, device=dev)
     status = torch.full((count,), -1, dtype=torch.int16, device=dev)
     batch.open_uniform(d_out, out_stride, d_plain, in_stride, count, n + 33, subkeys[0], 2, status)
     torch.cuda.synchronize()
     st = status.cpu().numpy().view(np.uint16)
     assert np.all(st & 0xff == 0)
-    assert np.array_equal(st >> 8, flags.cpu().numpy())
-    assert torch.equal(d_plain, d_in)
+    assert np.array_equal(st >> 8, fl)
+    plain = d_plain.cpu().numpy().reshape(count, in_stride)[:, :n]
+    assert np.array_equal(plain, hin[:count * in_stride].reshape(count, in_stride)[:, :n])
+
+
+@pytest.mark.parametrize("n,body_stride,pay_stride", [(4096, 4224, 4096), (100, 144, 112), (1000, 1040, 1008)])
+def test_uniform_open_rejections_in_a_full_wave(torch_dev, subkeys, L, n, body_stride, pay_stride):
+    """Rejected frames inside a cooperative (LDS-staged) wave: statuses per frame, the
+    other frames intact, rejected slots zeroed."""
+    torch, dev = torch_dev
+    from jeromq_amd import batch
+    count = 256
+    d_in = torch.empty(count * pay_stride, dtype=torch.uint8, device=dev)
+    batch.fill(d_in, 99 + n)
+    d_body = torch.zeros(count * body_stride, dtype=torch.uint8, device=dev)
+    batch.seal_uniform(d_in, pay_stride, d_body, body_stride, count, n, subkeys[0], 10)
+    torch.cuda.synchronize()
+    bodies = d_body.cpu().numpy().reshape(count, body_stride).copy()
+    bodies[5, 40] ^= 1                       # ciphertext -> CRYPTO
+    bodies[17, 3] ^= 0x20                    # "\x07MESsAGE" -> COMMAND
+    bodies[40, 8:16] = bodies[39, 8:16]      # nonce == previous -> SEQUENCE
+    bodies[63, 20] ^= 4                      # tag -> CRYPTO (last lane of wave 0)
+    bodies[64, 7] ^= 0x55                    # byte 7 is never compared (Msgs.java:31) -> OK
+    d_body = torch.from_numpy(bodies.reshape(-1)).to(dev)
+    d_plain = torch.full((count * pay_stride,), 0xEE, dtype=torch.uint8, device=dev)
+    status = torch.full((count,), -1, dtype=torch.int16, device=dev)
+    batch.open_uniform(d_body, body_stride, d_plain, pay_stride, count, n + 33, subkeys[0], 9, status)
+    torch.cuda.synchronize()
+    st = status.cpu().numpy().view(np.uint16) & 0xff
+    want = np.zeros(count, dtype=np.uint16)
+    want[[5, 63]] = L.CZ_STATUS_CRYPTO
+    want[17] = L.CZ_STATUS_COMMAND
+    want[40] = L.CZ_STATUS_SEQUENCE
+    assert np.array_equal(st, want), np.nonzero(st != want)
+    plain = d_plain.cpu().numpy().reshape(count, pay_stride)[:, :n]
+    ref = d_in.cpu().numpy().reshape(count, pay_stride)[:, :n]
+    ok = want == 0
+    assert np.array_equal(plain[ok], ref[ok])
+    rej = plain[~ok]
+    assert np.all((rej == 0) | (rej == 0xEE))  # never the plaintext
+    assert not np.array_equal(rej, ref[~ok])
 
 
 def test_nacl_box_afternm_golden(L, torch_dev):
@@ -360,7 +420,7 @@ def test_full_size_roundtrip(torch_dev, subkeys, count, n):
     torch, dev = torch_dev
     from jeromq_amd import batch
     in_stride = (n + 15) // 16 * 16
-    out_stride = (n + 33 + 15) // 16 * 16
+    out_stride = (n + 33 + 127) // 128 * 128 if n >= 1024 else (n + 33 + 15) // 16 * 16
     d_in = torch.empty(count * in_stride, dtype=torch.uint8, device=dev)
     batch.fill(d_in, 0x5EED0000 + n)
     d_out = torch.empty(count * out_stride, dtype=torch.uint8, device=dev)

@@ -1,0 +1,18 @@
+#!/bin/bash
+# Diagnostics session: instruction micro-benchmarks + seal-loop ablations + PMC passes.
+cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
+mkdir -p gpurun_out
+export TMPDIR=/tmp
+soft() { local rc=$1; [ "$rc" -lt 124 ]; }   # non-crash, non-timeout exit
+echo "== diag"
+timeout -k 10 300 ./tools/diag/diag > gpurun_out/diag.log 2>&1; rc=$?; cat gpurun_out/diag.log; soft $rc || exit $rc
+TAG=${1:-seal4k}
+ARGS=${2:---config 4k}
+i=0
+for pmc in "FETCH_SIZE" "WRITE_SIZE" "SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_ACTIVE_INST_VALU SQ_INSTS_VALU GRBM_GUI_ACTIVE" "SQ_INSTS_SALU SQ_INSTS_VMEM_RD SQ_INSTS_VMEM_WR SQ_BUSY_CYCLES TA_BUSY_avr TCP_TOTAL_CACHE_ACCESSES_sum" "TCC_HIT_sum TCC_MISS_sum TCC_EA0_RDREQ_sum TCC_EA0_WRREQ_sum"; do
+  i=$((i+1))
+  echo "== pmc pass $i: $pmc"
+  timeout -k 10 240 rocprofv3 --pmc $pmc --output-format csv -d gpurun_out/pmc_${TAG}_$i -o run --kernel-include-regex "k_seal|k_open" -- python3 bench.py --steps 2 --warmup 1 --no-cpu-baseline $ARGS > gpurun_out/pmc_${TAG}_$i.log 2>&1
+  rc=$?; tail -3 gpurun_out/pmc_${TAG}_$i.log; soft $rc || exit $rc
+done
+exit 0

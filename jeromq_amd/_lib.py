@@ -87,6 +87,7 @@ SIGNATURES = {
     "cz_last_error": (ctypes.c_char_p, []),
     "cz_version": (ctypes.c_char_p, []),
     "cz_device_ok": (_I, []),
+    "cz_tune": (_I, [ctypes.c_char_p, _I]),
 }
 
 _LIB = None

@@ -27,6 +27,7 @@ hipError_t czk_open_uniform(const void *, uint64_t, void *, uint64_t, uint32_t, 
 hipError_t czk_box_nacl(const void *, void *, uint32_t, const void *, uint64_t, int, int *, hipStream_t);
 hipError_t czk_subkeys(const void *, void *, uint32_t, const uint8_t *, hipStream_t);
 hipError_t czk_fill(void *, uint64_t, uint64_t, hipStream_t);
+int czk_tune(const char *, int);
 }
 
 namespace czi {
@@ -193,6 +194,14 @@ extern "C" {
 const char *cz_last_error(void) { return g_err.c_str(); }
 
 const char *cz_version(void) { return "curvezmq-mi355x 0.1 (gfx950)"; }
+
+int cz_tune(const char *key, int value)
+{
+    int old = czk_tune(key, value);
+    if (old < 0)
+        return fail(CZ_EINVAL, "cz_tune: unknown key");
+    return old;
+}
 
 int cz_device_ok(void)
 {

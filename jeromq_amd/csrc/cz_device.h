@@ -98,41 +98,47 @@ __device__ __forceinline__ void poly_init(Poly &P, u32 k0, u32 k1, u32 k2, u32 k
     P.h0 = P.h1 = P.h2 = P.h3 = P.h4 = 0;
 }
 
+__device__ __forceinline__ u32 addc(u32 a, u32 b, u32 cin, u32 &cout)
+{
+    return __builtin_addc(a, b, cin, &cout);
+}
+
+__device__ __forceinline__ u64 mad64(u32 a, u32 b, u64 c) { return (u64)a * b + c; }
+
+// h = (h + m + hibit*2^128) * r  (partially reduced).  Written as explicit 32-bit
+// carry chains (v_add_co_u32 / v_addc_co_u32) around 19 v_mad_u64_u32: the plain
+// u64 formulation compiled to zero-extension moves and 64-bit adds.
 __device__ __forceinline__ void poly_block(Poly &P, u32 m0, u32 m1, u32 m2, u32 m3, u32 hibit)
 {
-    u64 t;
-    t = (u64)P.h0 + m0;
-    u32 h0 = (u32)t;
-    t = (u64)P.h1 + m1 + (t >> 32);
-    u32 h1 = (u32)t;
-    t = (u64)P.h2 + m2 + (t >> 32);
-    u32 h2 = (u32)t;
-    t = (u64)P.h3 + m3 + (t >> 32);
-    u32 h3 = (u32)t;
-    u32 h4 = P.h4 + (u32)(t >> 32) + hibit;
+    u32 c;
+    const u32 h0 = addc(P.h0, m0, 0u, c);
+    const u32 h1 = addc(P.h1, m1, c, c);
+    const u32 h2 = addc(P.h2, m2, c, c);
+    const u32 h3 = addc(P.h3, m3, c, c);
+    const u32 h4 = P.h4 + c + hibit;
 
-    u64 d0 = (u64)h0 * P.r0 + (u64)h1 * P.s3 + (u64)h2 * P.s2 + (u64)h3 * P.s1;
-    u64 d1 = (u64)h0 * P.r1 + (u64)h1 * P.r0 + (u64)h2 * P.s3 + (u64)h3 * P.s2 + (u64)h4 * P.s1;
-    u64 d2 = (u64)h0 * P.r2 + (u64)h1 * P.r1 + (u64)h2 * P.r0 + (u64)h3 * P.s3 + (u64)h4 * P.s2;
-    u64 d3 = (u64)h0 * P.r3 + (u64)h1 * P.r2 + (u64)h2 * P.r1 + (u64)h3 * P.r0 + (u64)h4 * P.s3;
-    u32 h4r = h4 * P.r0;
+    const u64 d0 = mad64(h3, P.s1, mad64(h2, P.s2, mad64(h1, P.s3, mad64(h0, P.r0, 0))));
+    const u64 d1 = mad64(h4, P.s1, mad64(h3, P.s2, mad64(h2, P.s3, mad64(h1, P.r0, mad64(h0, P.r1, 0)))));
+    const u64 d2 = mad64(h4, P.s2, mad64(h3, P.s3, mad64(h2, P.r0, mad64(h1, P.r1, mad64(h0, P.r2, 0)))));
+    const u64 d3 = mad64(h4, P.s3, mad64(h3, P.r0, mad64(h2, P.r1, mad64(h1, P.r2, mad64(h0, P.r3, 0)))));
+    const u32 h4r = h4 * P.r0;
 
-    d1 += d0 >> 32;
-    d2 += d1 >> 32;
-    d3 += d2 >> 32;
-    h4 = h4r + (u32)(d3 >> 32);
-    // partial reduction: 2^130 == 5
-    u32 c = (h4 >> 2) + (h4 & ~3u);
-    h4 &= 3u;
-    t = (u64)(u32)d0 + c;
-    P.h0 = (u32)t;
-    t = (u64)(u32)d1 + (t >> 32);
-    P.h1 = (u32)t;
-    t = (u64)(u32)d2 + (t >> 32);
-    P.h2 = (u32)t;
-    t = (u64)(u32)d3 + (t >> 32);
-    P.h3 = (u32)t;
-    P.h4 = h4 + (u32)(t >> 32);
+    // propagate the column carries: h = d0 + d1*2^32 + d2*2^64 + d3*2^96 + h4r*2^128
+    const u32 e0 = (u32)d0;
+    const u32 e1 = addc((u32)d1, (u32)(d0 >> 32), 0u, c);
+    u32 t = (u32)(d1 >> 32) + c;
+    const u32 e2 = addc((u32)d2, t, 0u, c);
+    t = (u32)(d2 >> 32) + c;
+    const u32 e3 = addc((u32)d3, t, 0u, c);
+    const u32 e4 = (u32)(d3 >> 32) + c + h4r;
+    // partial reduction, 2^130 == 5: fold e4's bits above 2^130 back in
+    const u32 q = e4 >> 2;
+    const u32 k = q + (q << 2);
+    P.h0 = addc(e0, k, 0u, c);
+    P.h1 = addc(e1, 0u, c, c);
+    P.h2 = addc(e2, 0u, c, c);
+    P.h3 = addc(e3, 0u, c, c);
+    P.h4 = (e4 & 3u) + c;
 }
 
 // Final block of len bytes (1..15): bytes >= len cleared, byte len = 0x01, no 2^128 bit.

@@ -315,7 +315,13 @@ struct EmitRegion {
 // key = Salsa20 subkey (HSalsa20 already applied), nonce words from `counter`
 // (ZMQ: BE64 counter; NaCl: the caller passes n[16:24] read big-endian).
 // --------------------------------------------------------------------------
-template <int MODE, bool AL, class EM, bool PAIR = false>
+// UN0: the caller guarantees that the high nonce word (bswap of the counter's top
+// 32 bits) and the key are the same in every lane of the wave.  With the block
+// counter also wave-uniform, only state word 7 is per-lane when a block starts,
+// and the compiler's uniformity analysis moves everything that does not depend
+// on it -- 3 of the 4 first column quarter-rounds and 1 of the first row
+// quarter-rounds -- to the scalar unit (about 60 of the block's 960 VALU ops).
+template <int MODE, bool AL, class EM, bool PAIR = false, bool UN0 = false>
 __device__ __forceinline__ void seal_frame(const uint8_t *__restrict__ in, u32 n, u32 flags, u64 counter,
                                            const u32 key[8], EM &em)
 {
@@ -328,6 +334,8 @@ __device__ __forceinline__ void seal_frame(const uint8_t *__restrict__ in, u32 n
     const u64 inlen = n;
     u32 n0, n1;
     counter_nonce(counter, n0, n1);
+    if constexpr (UN0)
+        n0 = __builtin_amdgcn_readfirstlane(n0);
 
     u32 x[16], C[16];
     salsa20_block(x, key, n0, n1, 0u, 0u);
@@ -546,7 +554,7 @@ __device__ __forceinline__ void seal_frame(const uint8_t *__restrict__ in, u32 n
 // On a bad tag the emitted plaintext is overwritten with zeros (em.poison()).
 // Frames rejected before decryption emit nothing.
 // --------------------------------------------------------------------------
-template <int MODE, bool AL, class EM, bool PAIR = false>
+template <int MODE, bool AL, class EM, bool PAIR = false, bool UN0 = false>
 __device__ __forceinline__ u32 open_frame(const uint8_t *__restrict__ in, u32 size, const u32 key[8],
                                           bool check_floor, long long floor, u32 *flags_out, u64 *nonce_out,
                                           u64 nacl_counter, EM &em)
@@ -581,6 +589,8 @@ __device__ __forceinline__ u32 open_frame(const uint8_t *__restrict__ in, u32 si
     if (early != CZ_STATUS_OK && (!COOP || size < 33u))
         return early;  // cooperative callers only launch uniform sizes >= 33
     const bool dead = early != CZ_STATUS_OK;
+    if constexpr (UN0)
+        n0 = __builtin_amdgcn_readfirstlane(n0);  // caller checked: same in every lane
 
     const u32 mlen = size;
     const u32 nblk = (mlen + 63u) >> 6;
@@ -774,6 +784,12 @@ __device__ __forceinline__ bool aligned16(const void *a, const void *b)
     return (((uintptr_t)a | (uintptr_t)b) & 15u) == 0;
 }
 
+// true when v is the same in every active lane of the wave
+__device__ __forceinline__ bool wave_uniform(u32 v)
+{
+    return __builtin_amdgcn_ballot_w64(v != __builtin_amdgcn_readfirstlane(v)) == 0;
+}
+
 __device__ __forceinline__ u64 read_be64(const uint8_t *p)
 {
     u64 v = 0;
@@ -808,18 +824,26 @@ __global__ __launch_bounds__(BLOCK) void k_seal_uniform(const uint8_t *__restric
     const uint8_t *src = in + (uint64_t)i * in_stride;
     uint8_t *dst = out + (uint64_t)i * out_stride;
     const u32 mlen = len + 33u;
+    // high nonce word uniform over the wave (true unless the counters cross a 2^32 boundary)
+    const bool un0 = wave_uniform((u32)((counter0 + i) >> 32));
     if (ST != ST_DIRECT && full_wave) {
         const u32 fl = flags8 ? flags8[i] : 0u;
         const u32 lane = threadIdx.x & 63u;
         if constexpr (ST == ST_LINES) {
             EmitLines em{smem + (threadIdx.x >> 6) * (LINE_LDS_BYTES / 16), out + (uint64_t)wave_first * out_stride,
                          dst, out_stride, lane, mlen, 0u, true};
-            seal_frame<MODE_ZMQ, true, EmitLines, PAIR>(src, len, fl, counter0 + i, key, em);
+            if (un0)
+                seal_frame<MODE_ZMQ, true, EmitLines, PAIR, true>(src, len, fl, counter0 + i, key, em);
+            else
+                seal_frame<MODE_ZMQ, true, EmitLines, PAIR, false>(src, len, fl, counter0 + i, key, em);
         } else {
             const u32 st = (u32)out_stride;
             EmitRegion em{smem + (threadIdx.x >> 6) * ((64u * st) >> 4), out + (uint64_t)wave_first * out_stride, st,
                           lane, mlen};
-            seal_frame<MODE_ZMQ, true, EmitRegion, PAIR>(src, len, fl, counter0 + i, key, em);
+            if (un0)
+                seal_frame<MODE_ZMQ, true, EmitRegion, PAIR, true>(src, len, fl, counter0 + i, key, em);
+            else
+                seal_frame<MODE_ZMQ, true, EmitRegion, PAIR, false>(src, len, fl, counter0 + i, key, em);
         }
         return;
     }
@@ -923,15 +947,26 @@ __global__ __launch_bounds__(BLOCK) void k_open_uniform(const uint8_t *__restric
     if (ST != ST_DIRECT && full_wave) {
         long long floor = i > 0 ? (long long)read_be64(src - in_stride + 8) : (long long)floor0;
         const u32 lane = threadIdx.x & 63u;
+        const bool un0 = wave_uniform(*reinterpret_cast<const u32 *>(src + 8));
         if constexpr (ST == ST_LINES) {
             EmitLines em{smem + (threadIdx.x >> 6) * (LINE_LDS_BYTES / 16), out + (uint64_t)wave_first * out_stride,
                          dst, out_stride, lane, nout, 0u, false};
-            st = open_frame<MODE_ZMQ, true, EmitLines, PAIR>(src, size, key, check != 0, floor, &fl, &nonce, 0, em);
+            if (un0)
+                st = open_frame<MODE_ZMQ, true, EmitLines, PAIR, true>(src, size, key, check != 0, floor, &fl, &nonce,
+                                                                      0, em);
+            else
+                st = open_frame<MODE_ZMQ, true, EmitLines, PAIR, false>(src, size, key, check != 0, floor, &fl, &nonce,
+                                                                       0, em);
         } else {
             const u32 ost = (u32)out_stride;
             EmitRegion em{smem + (threadIdx.x >> 6) * ((64u * ost) >> 4), out + (uint64_t)wave_first * out_stride,
                           ost, lane, nout};
-            st = open_frame<MODE_ZMQ, true, EmitRegion, PAIR>(src, size, key, check != 0, floor, &fl, &nonce, 0, em);
+            if (un0)
+                st = open_frame<MODE_ZMQ, true, EmitRegion, PAIR, true>(src, size, key, check != 0, floor, &fl, &nonce,
+                                                                       0, em);
+            else
+                st = open_frame<MODE_ZMQ, true, EmitRegion, PAIR, false>(src, size, key, check != 0, floor, &fl,
+                                                                        &nonce, 0, em);
         }
         // rejected frames ran the loop as dead lanes: their slots hold zeros
         status[i] = (uint16_t)(st | (st == CZ_STATUS_OK ? (fl << 8) : 0u));

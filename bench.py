@@ -64,22 +64,33 @@ def barrier(world):
         dist.barrier()
 
 
-def max_over_ranks(world, x):
+def _reduce(world, x, op):
     if world == 1:
         return x
     import torch.distributed as dist
-    t = torch.tensor([x], dtype=torch.float64, device="cuda")
-    dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    dev = "cuda" if dist.get_backend() == "nccl" else "cpu"
+    t = torch.tensor([x], dtype=torch.float64, device=dev)
+    dist.all_reduce(t, op=op)
     return float(t.item())
+
+
+def max_over_ranks(world, x):
+    """slowest rank's time (the contract's max over ranks)"""
+    import torch.distributed as dist
+    return _reduce(world, x, dist.ReduceOp.MAX if world > 1 else None)
 
 
 def sum_over_ranks(world, x):
-    if world == 1:
-        return x
     import torch.distributed as dist
-    t = torch.tensor([x], dtype=torch.float64, device="cuda")
-    dist.all_reduce(t, op=dist.ReduceOp.SUM)
-    return float(t.item())
+    return _reduce(world, x, dist.ReduceOp.SUM if world > 1 else None)
+
+
+def shard_plan(rank, frames_per_rank, cfg="4k"):
+    """Rank r seals frames [r*F, (r+1)*F) of the global batch: nonce counters 3 + r*F ..,
+    its own payload seed.  Frames are independent, so no data crosses ranks (weak scaling)."""
+    counter0 = 3 + rank * frames_per_rank
+    seed = 0x5EED0000 + {"4k": 1, "100b": 2, "zipf": 3, "open4k": 4}[cfg] + 1000 * rank
+    return counter0, seed
 
 
 class Workload:
@@ -90,9 +101,8 @@ class Workload:
         self.dev = dev
         key = torch.tensor(list(PRECOM), dtype=torch.uint8, device=dev).view(1, 32)
         self.subkey = batch.subkeys(key, _lib.CZ_DIR_C2S)[0].contiguous()
-        self.counter0 = 3 + rank * frames
+        self.counter0, seed = shard_plan(rank, frames, cfg)
         self.count = frames
-        seed = 0x5EED0000 + {"4k": 1, "100b": 2, "zipf": 3, "open4k": 4}[cfg] + 1000 * rank
         if cfg in ("4k", "100b", "open4k"):
             n = 4096 if cfg != "100b" else 100
             self.n = n

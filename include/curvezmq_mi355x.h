@@ -198,7 +198,8 @@ const char *cz_version(void);
 /* 1 if a HIP device is present and the gfx950 code object loaded */
 int cz_device_ok(void);
 /* Kernel-variant knob for A/B measurement; returns the previous value or CZ_EINVAL.
- *   "pair": 1 = uniform kernels read whole 128-byte input lines per two blocks (default), 0 = per block */
+ *   "pair": 1 = uniform kernels read whole 128-byte input lines per two blocks (default), 0 = per block
+ *   "un0":  1 = scalar first Salsa round when the high nonce word is wave-uniform (default), 0 = off */
 int cz_tune(const char *key, int value);
 
 #ifdef __cplusplus

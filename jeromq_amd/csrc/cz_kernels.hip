@@ -811,7 +811,7 @@ __global__ __launch_bounds__(BLOCK) void k_seal_uniform(const uint8_t *__restric
                                                          uint8_t *__restrict__ out, uint64_t out_stride,
                                                          uint32_t count, uint32_t len,
                                                          const uint8_t *__restrict__ subkey, uint64_t counter0,
-                                                         const uint8_t *__restrict__ flags8)
+                                                         const uint8_t *__restrict__ flags8, int allow_un0)
 {
     extern __shared__ uint4 smem[];
     const uint32_t i = blockIdx.x * BLOCK + threadIdx.x;
@@ -825,7 +825,7 @@ __global__ __launch_bounds__(BLOCK) void k_seal_uniform(const uint8_t *__restric
     uint8_t *dst = out + (uint64_t)i * out_stride;
     const u32 mlen = len + 33u;
     // high nonce word uniform over the wave (true unless the counters cross a 2^32 boundary)
-    const bool un0 = wave_uniform((u32)((counter0 + i) >> 32));
+    const bool un0 = allow_un0 && wave_uniform((u32)((counter0 + i) >> 32));
     if (ST != ST_DIRECT && full_wave) {
         const u32 fl = flags8 ? flags8[i] : 0u;
         const u32 lane = threadIdx.x & 63u;
@@ -928,7 +928,7 @@ __global__ __launch_bounds__(BLOCK) void k_open_uniform(const uint8_t *__restric
                                                          uint8_t *__restrict__ out, uint64_t out_stride,
                                                          uint32_t count, uint32_t size,
                                                          const uint8_t *__restrict__ subkey, uint64_t floor0,
-                                                         int check, uint16_t *__restrict__ status)
+                                                         int check, uint16_t *__restrict__ status, int allow_un0)
 {
     extern __shared__ uint4 smem[];
     const uint32_t i = blockIdx.x * BLOCK + threadIdx.x;
@@ -947,7 +947,7 @@ __global__ __launch_bounds__(BLOCK) void k_open_uniform(const uint8_t *__restric
     if (ST != ST_DIRECT && full_wave) {
         long long floor = i > 0 ? (long long)read_be64(src - in_stride + 8) : (long long)floor0;
         const u32 lane = threadIdx.x & 63u;
-        const bool un0 = wave_uniform(*reinterpret_cast<const u32 *>(src + 8));
+        const bool un0 = allow_un0 && wave_uniform(*reinterpret_cast<const u32 *>(src + 8));
         if constexpr (ST == ST_LINES) {
             EmitLines em{smem + (threadIdx.x >> 6) * (LINE_LDS_BYTES / 16), out + (uint64_t)wave_first * out_stride,
                          dst, out_stride, lane, nout, 0u, false};
@@ -1082,6 +1082,7 @@ int pick_staging(uint64_t stride, uint32_t out_bytes, bool aligned)
 
 // run-time tuning knobs (cz_tune): whole-line input loads for the uniform kernels
 static int g_pair = 1;
+static int g_un0 = 1;  // scalar first Salsa round when the high nonce word is wave-uniform
 
 // ---------------------------------------------------------------------------
 // Launchers (called from cz_host.cpp).  No allocation, no synchronisation:
@@ -1099,7 +1100,7 @@ hipError_t czk_seal_uniform(const void *in, uint64_t in_stride, void *out, uint6
     const bool al = ((((uintptr_t)in | (uintptr_t)out | in_stride | out_stride) & 15u) == 0);
 #define CZ_SEAL_LAUNCH(ST, PR, LDS)                                                                        \
     hipLaunchKernelGGL((k_seal_uniform<ST, PR>), grid, dim3(BLOCK), (LDS), s, (const uint8_t *)in, in_stride,   \
-                       (uint8_t *)out, out_stride, count, len, (const uint8_t *)subkey, counter0, flags8)
+                       (uint8_t *)out, out_stride, count, len, (const uint8_t *)subkey, counter0, flags8, g_un0)
     const int st = pick_staging(out_stride, len + 33u, al);
     const unsigned lds = st == ST_LINES ? WAVES * LINE_LDS_BYTES : (st == ST_REGION ? (unsigned)(WAVES * 64 * out_stride) : 0u);
     // whole-line input pays for large frames (A/B: 4 KiB seal 2.34 vs 2.51 ms) but
@@ -1149,7 +1150,7 @@ hipError_t czk_open_uniform(const void *in, uint64_t in_stride, void *out, uint6
     const uint32_t nout = size >= 33u ? size - 33u : 0u;
 #define CZ_OPEN_LAUNCH(ST, PR, LDS)                                                                        \
     hipLaunchKernelGGL((k_open_uniform<ST, PR>), grid, dim3(BLOCK), (LDS), s, (const uint8_t *)in, in_stride,   \
-                       (uint8_t *)out, out_stride, count, size, (const uint8_t *)subkey, floor0, check, status)
+                       (uint8_t *)out, out_stride, count, size, (const uint8_t *)subkey, floor0, check, status, g_un0)
     const int st = size >= 33u ? pick_staging(out_stride, nout, al) : (int)ST_DIRECT;
     const unsigned lds = st == ST_LINES ? WAVES * LINE_LDS_BYTES : (st == ST_REGION ? (unsigned)(WAVES * 64 * out_stride) : 0u);
     if (g_pair && st != ST_REGION) {
@@ -1193,6 +1194,11 @@ int czk_tune(const char *key, int value)
     if (key[0] == 'p' && key[1] == 'a' && key[2] == 'i' && key[3] == 'r' && key[4] == 0) {
         int old = g_pair;
         g_pair = value != 0;
+        return old;
+    }
+    if (key[0] == 'u' && key[1] == 'n' && key[2] == '0' && key[3] == 0) {
+        int old = g_un0;
+        g_un0 = value != 0;
         return old;
     }
     return -1;

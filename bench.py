@@ -38,7 +38,7 @@ def parse():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=3)
-    ap.add_argument("--config", default="4k", choices=["4k", "100b", "zipf", "open4k"])
+    ap.add_argument("--config", default="4k", choices=["4k", "100b", "zipf", "open4k", "e2e4k"])
     ap.add_argument("--frames", type=int, default=FRAMES)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-seconds", type=float, default=10.0, help="target CPU-baseline sample duration")
@@ -232,6 +232,61 @@ def cpu_baseline(wl, target_s):
                       f"{os.cpu_count()} logical CPUs visible"}
 
 
+def e2e_host(args, dev):
+    """End-to-end from pinned host memory (the JNI path): H2D + seal + D2H pipelined over 3
+    streams by cz_ctx_seal_uniform, then the reverse open.  Wall clock, payload GiB/s."""
+    import ctypes
+    lib = _lib.lib()
+    frames = min(args.frames, 1 << 18)
+    n = 4096
+    in_stride, out_stride = 4096, 4224
+    pin = lib.cz_host_alloc(frames * in_stride)
+    pout = lib.cz_host_alloc(frames * out_stride)
+    pback = lib.cz_host_alloc(frames * in_stride)
+    pstat = lib.cz_host_alloc(2 * frames)
+    if not (pin and pout and pback and pstat):
+        raise SystemExit("cz_host_alloc failed: " + _lib.last_error())
+    hin = np.ctypeslib.as_array((ctypes.c_uint8 * (frames * in_stride)).from_address(pin))
+    hin[:] = np.frombuffer(np.random.default_rng(7).bytes(frames * in_stride), dtype=np.uint8)
+    ctx = ctypes.c_void_p()
+    _lib.check(lib.cz_ctx_create(ctypes.byref(ctx), dev.index or 0), "cz_ctx_create")
+    _lib.check(lib.cz_ctx_set_keys(ctx, PRECOM, 1, _lib.CZ_DIR_C2S), "cz_ctx_set_keys")
+    chunk = 16384
+    res = {}
+    for name, fn in (("seal", lambda: lib.cz_ctx_seal_uniform(ctx, frames, n, pin, in_stride, pout, out_stride, 3,
+                                                               None, chunk)),
+                     ("open", lambda: lib.cz_ctx_open_uniform(ctx, frames, n + 33, pout, out_stride, pback, in_stride,
+                                                               2, 1, pstat, chunk))):
+        _lib.check(fn(), name)  # warm-up (allocates the per-stream buffers)
+        ts = []
+        for _ in range(max(args.steps // 4, 3)):
+            t0 = time.perf_counter()
+            _lib.check(fn(), name)
+            ts.append(time.perf_counter() - t0)
+        res[name] = float(np.median(ts))
+    sys.path.insert(0, os.path.join(ROOT, "tests"))
+    from cz_testlib import or_curve_encode
+    hout = np.ctypeslib.as_array((ctypes.c_uint8 * (frames * out_stride)).from_address(pout))
+    for i in (0, frames - 1):
+        body = hout[i * out_stride:i * out_stride + n + 33].tobytes()
+        if body != or_curve_encode(hin[i * in_stride:i * in_stride + n].tobytes(), 0, 3 + i, 0, PRECOM):
+            raise SystemExit(f"e2e parity failure at frame {i}")
+    hback = np.ctypeslib.as_array((ctypes.c_uint8 * (frames * in_stride)).from_address(pback))
+    st = np.ctypeslib.as_array((ctypes.c_uint16 * frames).from_address(pstat))
+    if np.any(st & 0xff) or not np.array_equal(hback, hin):
+        raise SystemExit("e2e open round trip failed")
+    lib.cz_ctx_destroy(ctx)
+    for p in (pin, pout, pback, pstat):
+        lib.cz_host_free(p)
+    pay = frames * n
+    return {"metric": "CURVE seal GiB/s end-to-end from pinned host memory (H2D + seal + D2H), 4 KiB frames",
+            "value": round(pay / res["seal"] / 2**30, 3), "unit": "GiB/s", "n_gpus": 1,
+            "open_GiBps": round(pay / res["open"] / 2**30, 3),
+            "pcie_bytes_per_s": round((frames * (in_stride + out_stride)) / res["seal"] / 1e9, 2),
+            "config": {"workload": f"{frames} x 4 KiB frames, pinned host buffers, 3-stream pipeline, "
+                                   f"{chunk}-frame chunks", "frames": frames}}
+
+
 def load_pmc_traffic(cfg):
     """HBM bytes per launch from the committed rocprofv3 PMC summary, if one exists for this config."""
     path = os.path.join(ROOT, "profiles", "pmc_traffic.json")
@@ -250,6 +305,11 @@ def main():
     args = parse()
     world, rank, local = setup_dist(args)
     dev = torch.device(f"cuda:{local}")
+    if args.config == "e2e4k":
+        line = e2e_host(args, dev)
+        if rank == 0:
+            print(json.dumps(line), flush=True)
+        return
     wl = Workload(args.config, args.frames, rank, dev)
 
     for _ in range(args.warmup):

@@ -74,6 +74,8 @@ SIGNATURES = {
     "cz_ctx_set_keys": (_I, [_VP, _VP, _U32, _I]),
     "cz_ctx_seal": (_I, [_VP, _VP, _U32, _VP, _U64, _VP, _U64]),
     "cz_ctx_open": (_I, [_VP, _VP, _U32, _VP, _U64, _VP, _U64, _VP]),
+    "cz_ctx_seal_uniform": (_I, [_VP, _U32, _U32, _VP, _U64, _VP, _U64, _U64, _VP, _U32]),
+    "cz_ctx_open_uniform": (_I, [_VP, _U32, _U32, _VP, _U64, _VP, _U64, _U64, _I, _VP, _U32]),
     "cz_host_alloc": (_VP, [_U64]),
     "cz_host_free": (None, [_VP]),
     "cz_mech_create": (_VP, [_I, _VP, _U64, _U64, _I]),

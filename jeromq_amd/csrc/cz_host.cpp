@@ -187,6 +187,10 @@ struct cz_ctx {
     DevBuf desc, in, out, status, keys, subkeys;
     HostBuf hdesc;
     uint32_t nkeys = 0;
+    // pipelined uniform batches: PIPE streams, each with its own chunk buffers
+    static constexpr int PIPE = 3;
+    hipStream_t ps[PIPE] = {nullptr, nullptr, nullptr};
+    DevBuf pin[PIPE], pout[PIPE], pflags[PIPE], pstatus[PIPE];
 };
 
 extern "C" {
@@ -363,6 +367,16 @@ void cz_ctx_destroy(cz_ctx *c)
     c->keys.release();
     c->subkeys.release();
     c->hdesc.release();
+    for (int k = 0; k < cz_ctx::PIPE; k++) {
+        if (c->ps[k]) {
+            (void)hipStreamSynchronize(c->ps[k]);
+            (void)hipStreamDestroy(c->ps[k]);
+        }
+        c->pin[k].release();
+        c->pout[k].release();
+        c->pflags[k].release();
+        c->pstatus[k].release();
+    }
     (void)hipStreamDestroy(c->stream);
     delete c;
 }
@@ -455,6 +469,98 @@ int cz_ctx_open(cz_ctx *c, const cz_frame_desc *h_desc, uint32_t count, const vo
                 void *h_out, uint64_t out_bytes, uint16_t *h_status)
 {
     return ctx_run(c, h_desc, count, h_in, in_bytes, h_out, out_bytes, h_status, false);
+}
+
+// Pipelined host-staged uniform batch: chunk k of `chunk` frames runs
+// H2D -> kernel -> D2H on stream k % PIPE with that stream's buffers, so PCIe
+// transfers in both directions overlap each other and the kernels.
+static int ctx_uniform(cz_ctx *c, bool seal, uint32_t count, uint32_t len, const void *h_in, uint64_t in_stride,
+                       void *h_out, uint64_t out_stride, uint64_t counter0, const uint8_t *h_flags8,
+                       uint16_t *h_status, int check, uint32_t chunk)
+{
+    if (!c || (count && (!h_in || !h_out)))
+        return fail(CZ_EINVAL, "cz_ctx_*_uniform: null pointer");
+    if (c->nkeys < 1)
+        return fail(CZ_EINVAL, "cz_ctx_*_uniform: no key (cz_ctx_set_keys)");
+    if (!seal && count && !h_status)
+        return fail(CZ_EINVAL, "cz_ctx_open_uniform: null status");
+    const uint64_t olen = seal ? (uint64_t)len + CZ_MESSAGE_OVERHEAD : (len >= 33 ? len - 33u : 0u);
+    if (count > 1 && (in_stride < len || out_stride < olen))
+        return fail(CZ_EINVAL, "cz_ctx_*_uniform: stride smaller than a frame");
+    if (count == 0)
+        return CZ_OK;
+    if (chunk == 0)
+        chunk = 16384;
+    hipError_t e;
+    (void)hipSetDevice(c->device);
+    const uint32_t per = chunk < count ? chunk : count;
+    for (int k = 0; k < cz_ctx::PIPE; k++) {
+        if (!c->ps[k] && (e = hipStreamCreateWithFlags(&c->ps[k], hipStreamNonBlocking)) != hipSuccess)
+            return hip_fail(e, "hipStreamCreate");
+        if ((e = c->pin[k].reserve((uint64_t)per * in_stride + 16)) != hipSuccess ||
+            (e = c->pout[k].reserve((uint64_t)per * out_stride + 16)) != hipSuccess ||
+            (e = c->pflags[k].reserve(per)) != hipSuccess || (e = c->pstatus[k].reserve(2ull * per)) != hipSuccess)
+            return hip_fail(e, "hipMalloc");
+    }
+    const uint8_t *hin = (const uint8_t *)h_in;
+    uint8_t *hout = (uint8_t *)h_out;
+    uint32_t k = 0;
+    for (uint32_t f0 = 0; f0 < count; f0 += per, k++) {
+        const uint32_t nc = count - f0 < per ? count - f0 : per;
+        const int q = k % cz_ctx::PIPE;
+        hipStream_t st = c->ps[q];
+        const uint64_t ib = (uint64_t)(nc - 1) * in_stride + len;
+        if ((e = hipMemcpyAsync(c->pin[q].ptr, hin + (uint64_t)f0 * in_stride, ib, hipMemcpyHostToDevice, st)) !=
+            hipSuccess)
+            return hip_fail(e, "H2D");
+        if (seal) {
+            const uint8_t *dfl = nullptr;
+            if (h_flags8) {
+                if ((e = hipMemcpyAsync(c->pflags[q].ptr, h_flags8 + f0, nc, hipMemcpyHostToDevice, st)) != hipSuccess)
+                    return hip_fail(e, "H2D flags");
+                dfl = (const uint8_t *)c->pflags[q].ptr;
+            }
+            e = czk_seal_uniform(c->pin[q].ptr, in_stride, c->pout[q].ptr, out_stride, nc, len, c->subkeys.ptr,
+                                 counter0 + f0, dfl, st);
+        } else {
+            // the chunk's first frame must beat the previous chunk's last nonce: read it from the host copy
+            uint64_t floor0 = counter0;
+            if (f0 > 0) {
+                const uint8_t *pb = hin + (uint64_t)(f0 - 1) * in_stride + 8;
+                floor0 = 0;
+                for (int b = 0; b < 8; b++)
+                    floor0 = (floor0 << 8) | pb[b];
+            }
+            e = czk_open_uniform(c->pin[q].ptr, in_stride, c->pout[q].ptr, out_stride, nc, len, c->subkeys.ptr, floor0,
+                                 check, (uint16_t *)c->pstatus[q].ptr, st);
+        }
+        if (e != hipSuccess)
+            return hip_fail(e, "launch");
+        if ((e = hipMemcpyAsync(hout + (uint64_t)f0 * out_stride, c->pout[q].ptr, (uint64_t)nc * out_stride,
+                                hipMemcpyDeviceToHost, st)) != hipSuccess)
+            return hip_fail(e, "D2H");
+        if (!seal && (e = hipMemcpyAsync(h_status + f0, c->pstatus[q].ptr, 2ull * nc, hipMemcpyDeviceToHost, st)) !=
+                         hipSuccess)
+            return hip_fail(e, "D2H status");
+    }
+    for (int q = 0; q < cz_ctx::PIPE; q++)
+        if ((e = hipStreamSynchronize(c->ps[q])) != hipSuccess)
+            return hip_fail(e, "sync");
+    return CZ_OK;
+}
+
+int cz_ctx_seal_uniform(cz_ctx *c, uint32_t count, uint32_t len, const void *h_in, uint64_t in_stride, void *h_out,
+                        uint64_t out_stride, uint64_t counter0, const uint8_t *h_flags8, uint32_t chunk_frames)
+{
+    return ctx_uniform(c, true, count, len, h_in, in_stride, h_out, out_stride, counter0, h_flags8, nullptr, 0,
+                       chunk_frames);
+}
+
+int cz_ctx_open_uniform(cz_ctx *c, uint32_t count, uint32_t size, const void *h_in, uint64_t in_stride, void *h_out,
+                        uint64_t out_stride, uint64_t floor0, int check, uint16_t *h_status, uint32_t chunk_frames)
+{
+    return ctx_uniform(c, false, count, size, h_in, in_stride, h_out, out_stride, floor0, nullptr, h_status, check,
+                       chunk_frames);
 }
 
 void *cz_host_alloc(uint64_t bytes)

@@ -414,6 +414,41 @@ def test_ctx_host_staged(L, torch_dev):
         lib.cz_ctx_destroy(ctx)
 
 
+def test_ctx_pipelined_uniform(L, torch_dev):
+    """Host-staged pipelined seal/open (3 streams, chunks) vs the oracle; chunk boundaries
+    carry the replay floor across chunks."""
+    lib = L.lib()
+    ctx = ctypes.c_void_p()
+    L.check(lib.cz_ctx_create(ctypes.byref(ctx), 0))
+    try:
+        L.check(lib.cz_ctx_set_keys(ctx, PRECOM, 1, L.CZ_DIR_C2S))
+        count, n, ist, ost = 1000, 300, 304, 384
+        hin = np.frombuffer(splitmix_bytes(count * ist, 1234), dtype=np.uint8).copy()
+        flags = (np.arange(count) % 3).astype(np.uint8)
+        hout = np.zeros(count * ost, dtype=np.uint8)
+        L.check(lib.cz_ctx_seal_uniform(ctx, count, n, hin.ctypes.data, ist, hout.ctypes.data, ost, 7,
+                                        flags.ctypes.data, 96))
+        for i in (0, 95, 96, 500, count - 1):
+            body = hout[i * ost:i * ost + n + 33].tobytes()
+            assert body == or_curve_encode(hin[i * ist:i * ist + n].tobytes(), int(flags[i]), 7 + i, 0, PRECOM)
+        back = np.zeros(count * ist, dtype=np.uint8)
+        st = np.zeros(count, dtype=np.uint16)
+        L.check(lib.cz_ctx_set_keys(ctx, PRECOM, 1, L.CZ_DIR_C2S))
+        L.check(lib.cz_ctx_open_uniform(ctx, count, n + 33, hout.ctypes.data, ost, back.ctypes.data, ist, 6, 1,
+                                        st.ctypes.data, 96))
+        assert not np.any(st & 0xff)
+        assert np.array_equal(st >> 8, flags)
+        assert np.array_equal(back.reshape(count, ist)[:, :n], hin.reshape(count, ist)[:, :n])
+        # a replayed frame at a chunk boundary is caught with the floor carried across chunks
+        hout2 = hout.copy()
+        hout2[96 * ost + 8:96 * ost + 16] = hout2[95 * ost + 8:95 * ost + 16]
+        L.check(lib.cz_ctx_open_uniform(ctx, count, n + 33, hout2.ctypes.data, ost, back.ctypes.data, ist, 6, 1,
+                                        st.ctypes.data, 96))
+        assert (st[96] & 0xff) == L.CZ_STATUS_SEQUENCE and not np.any(st[:96] & 0xff)
+    finally:
+        lib.cz_ctx_destroy(ctx)
+
+
 @pytest.mark.parametrize("count,n", [(1 << 20, 100), (1 << 20, 4096)])
 def test_full_size_roundtrip(torch_dev, subkeys, count, n):
     """BASELINE configs 2 and 3 at full size: seal -> open round trip, sampled frames vs oracle."""

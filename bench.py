@@ -8,7 +8,7 @@ framing, CurveClientMechanism.java:126-163).  One connection direction (C->S,
 the RFC test keys of org/zeromq/ZMQ.java:4603-4624), counters 3.., every 8th
 frame MORE.  Payload bytes: counter-based SplitMix64, generated on device.
 
-  python bench.py [--gpus N] [--steps K] [--warmup W] [--config 4k|100b|zipf|open4k]
+  python bench.py [--gpus N] [--steps K] [--warmup W] [--config 4k|100b|zipf|zipf_lane|open4k|e2e4k]
 
 N > 1 (torch.distributed.run, one rank per GPU): every rank seals its own 2^20
 frames (counters offset by rank * 2^20): no collective on the timed path ("weak").
@@ -38,7 +38,7 @@ def parse():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=3)
-    ap.add_argument("--config", default="4k", choices=["4k", "100b", "zipf", "open4k", "e2e4k"])
+    ap.add_argument("--config", default="4k", choices=["4k", "100b", "zipf", "zipf_lane", "open4k", "e2e4k"])
     ap.add_argument("--frames", type=int, default=FRAMES)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-seconds", type=float, default=10.0, help="target CPU-baseline sample duration")
@@ -89,7 +89,7 @@ def shard_plan(rank, frames_per_rank, cfg="4k"):
     """Rank r seals frames [r*F, (r+1)*F) of the global batch: nonce counters 3 + r*F ..,
     its own payload seed.  Frames are independent, so no data crosses ranks (weak scaling)."""
     counter0 = 3 + rank * frames_per_rank
-    seed = 0x5EED0000 + {"4k": 1, "100b": 2, "zipf": 3, "open4k": 4}[cfg] + 1000 * rank
+    seed = 0x5EED0000 + {"4k": 1, "100b": 2, "zipf": 3, "zipf_lane": 3, "open4k": 4}[cfg] + 1000 * rank
     return counter0, seed
 
 
@@ -153,10 +153,15 @@ class Workload:
             batch.fill(self.d_in, seed)
             self.d_out = torch.empty(out_bytes, dtype=torch.uint8, device=dev)
             self.d_desc = torch.from_numpy(desc.view(np.uint8)).to(dev)
-            order = batch.plan_order(desc)
-            self.d_order = torch.from_numpy(order.view(np.int32)).to(dev)
             self.payload_bytes = in_bytes
-            self.read_bytes = in_bytes + 40 * frames + 4 * frames
+            if cfg == "zipf":
+                # long frames split into 64-block segments (one lane each) + Poly1305 combine
+                self.plan = batch.SegmentPlan(desc, open_=False).to(dev)
+                self.read_bytes = in_bytes + 40 * frames + 16 * self.plan.nseg + 16 * self.plan.ncomb
+            else:  # zipf_lane: one lane per frame, longest first
+                order = batch.plan_order(desc)
+                self.d_order = torch.from_numpy(order.view(np.int32)).to(dev)
+                self.read_bytes = in_bytes + 40 * frames + 4 * frames
             self.write_bytes = int((lens + np.uint64(33)).sum())
             self.n = None
         torch.cuda.synchronize()
@@ -168,6 +173,8 @@ class Workload:
         elif self.cfg == "open4k":
             batch.open_uniform(self.d_out, self.out_stride, self.d_plain, self.in_stride, self.count, self.n + 33,
                                self.subkey, self.counter0 - 1, self.status)
+        elif self.cfg == "zipf":
+            batch.seal_segments(self.d_desc, self.plan, self.d_in, self.d_out, self.subkey.view(1, 32))
         else:
             batch.seal_batch(self.d_desc, self.count, self.d_in, self.d_out, self.subkey.view(1, 32),
                              order=self.d_order)
@@ -191,7 +198,8 @@ class Workload:
             if not torch.equal(self.d_plain, self.d_in):
                 raise SystemExit("open round trip mismatch")
         else:
-            for i in (0, 1, self.count - 1):
+            longest = int(np.argmax(self.desc_np["len"]))
+            for i in (0, 1, longest, self.count - 1):
                 d = self.desc_np[i]
                 p = self.d_in[int(d["in_off"]):int(d["in_off"]) + int(d["len"])].cpu().numpy().tobytes()
                 body = self.d_out[int(d["out_off"]):int(d["out_off"]) + int(d["len"]) + 33].cpu().numpy().tobytes()
@@ -345,7 +353,8 @@ def main():
 
     if rank == 0:
         names = {"4k": "1M x 4 KiB frames, seal (configs[1])", "100b": "1M x 100 B frames, seal (configs[2])",
-                 "zipf": "1M Zipf(1.2) 64 B..64 KiB frames, seal (configs[3])",
+                 "zipf": "1M Zipf(1.2) 64 B..64 KiB frames, seal, segmented (configs[3])",
+                 "zipf_lane": "1M Zipf(1.2) 64 B..64 KiB frames, seal, lane per frame (configs[3])",
                  "open4k": "1M x 4 KiB frames, open+verify (configs[4] leg)"}
         line = {
             "metric": "CURVE encrypt+MAC GiB/s (device-resident), batched 4 KiB frames, 1/2/4/8 GPU",

@@ -140,6 +140,38 @@ int cz_open_uniform(uint32_t count, uint32_t size, const void *d_in, uint64_t in
 /* Host-side planner: order[] = frame indices sorted by decreasing len (stable). */
 int cz_plan_order(const cz_frame_desc *h_desc, uint32_t count, uint32_t *h_order);
 
+/* ---- 3b. segmented (ragged) batches ---------------------------------------------
+ * One lane per frame makes a long frame the batch's critical path (a 64 KiB frame is
+ * 1025 sequential Salsa20 blocks on one lane).  cz_plan_segments splits frames longer
+ * than 1.5 x seg_blocks 64-byte blocks into seg_blocks-block segments (the last one
+ * takes the remainder, 1..seg_blocks blocks), sorts segments longest first, and lists the split frames for
+ * the combine step, which joins the per-segment Poly1305 partials with r^m powers.
+ * d_work must hold 64 bytes per part (*npart from the planner).  Output contract as
+ * cz_seal_batch / cz_open_batch (statuses, nonces, zeroed plaintext on a bad tag). */
+typedef struct cz_segment {
+    uint32_t frame;       /* index into the descriptor array */
+    uint32_t first_block; /* first 64-byte box block of the segment */
+    uint32_t nblocks;
+    uint32_t part;        /* partial-record index, 0xffffffff for a frame in one segment */
+} cz_segment;
+typedef struct cz_combine {
+    uint32_t frame;
+    uint32_t part0; /* first partial record of the frame (its segments are consecutive) */
+    uint32_t nseg;
+    uint32_t reserved;
+} cz_combine;
+/* open = 0: desc.len is a payload length (seal); 1: a body size (open).  Returns CZ_EINVAL
+ * with *nseg / *ncomb set to the sizes needed when a capacity is too small. */
+int cz_plan_segments(const cz_frame_desc *h_desc, uint32_t count, int open, uint32_t seg_blocks, cz_segment *h_seg,
+                     uint32_t seg_cap, uint32_t *nseg, cz_combine *h_comb, uint32_t comb_cap, uint32_t *ncomb,
+                     uint32_t *npart);
+int cz_seal_segments(const cz_frame_desc *d_desc, const cz_segment *d_seg, uint32_t nseg, const cz_combine *d_comb,
+                     uint32_t ncomb, const void *d_in, void *d_out, const void *d_subkeys, void *d_work,
+                     void *stream);
+int cz_open_segments(const cz_frame_desc *d_desc, const cz_segment *d_seg, uint32_t nseg, const cz_combine *d_comb,
+                     uint32_t ncomb, const void *d_in, void *d_out, const void *d_subkeys, void *d_work,
+                     uint16_t *d_status, uint64_t *d_nonces, void *stream);
+
 /* Synthetic data: fill d_buf with the counter-based SplitMix64 byte stream (seed). */
 int cz_fill(void *d_buf, uint64_t nbytes, uint64_t seed, void *stream);
 

@@ -4,6 +4,8 @@ All functions launch asynchronously on `stream` (default: torch's current
 stream) and return immediately; the crypto runs in the gfx950 kernels of
 libcurvezmq_mi355x.so.
 """
+import ctypes
+
 import numpy as np
 
 from . import _lib
@@ -115,3 +117,60 @@ def plan_order(desc_np):
 
 DESC_DTYPE = np.dtype([("in_off", "<u8"), ("out_off", "<u8"), ("len", "<u4"), ("key_idx", "<u4"),
                        ("counter", "<u8"), ("flags", "<u4"), ("prev", "<i4")])
+
+SEGMENT_DTYPE = np.dtype([("frame", "<u4"), ("first_block", "<u4"), ("nblocks", "<u4"), ("part", "<u4")])
+COMBINE_DTYPE = np.dtype([("frame", "<u4"), ("part0", "<u4"), ("nseg", "<u4"), ("reserved", "<u4")])
+SEG_BLOCKS = 64  # 4 KiB of box per lane: balances Zipf batches whose frames reach 64 KiB
+
+
+class SegmentPlan:
+    """Host plan for a ragged batch: frames longer than 1.5 x seg_blocks are split
+    into seg_blocks-block segments (cz_plan_segments).  `to(device)` uploads the
+    segment and combine lists and allocates the partial-record workspace."""
+
+    def __init__(self, desc_np, open_=False, seg_blocks=SEG_BLOCKS):
+        d = np.ascontiguousarray(desc_np)
+        count = len(d)
+        nseg, ncomb, npart = ctypes.c_uint32(), ctypes.c_uint32(), ctypes.c_uint32()
+        L = _lib.lib()
+        L.cz_plan_segments(d.ctypes.data, count, int(open_), seg_blocks, None, 0, ctypes.byref(nseg), None, 0,
+                           ctypes.byref(ncomb), ctypes.byref(npart))
+        self.segments = np.zeros(max(nseg.value, 1), dtype=SEGMENT_DTYPE)
+        self.combines = np.zeros(max(ncomb.value, 1), dtype=COMBINE_DTYPE)
+        _lib.check(L.cz_plan_segments(d.ctypes.data, count, int(open_), seg_blocks, self.segments.ctypes.data,
+                                      len(self.segments), ctypes.byref(nseg), self.combines.ctypes.data,
+                                      len(self.combines), ctypes.byref(ncomb), ctypes.byref(npart)),
+                   "cz_plan_segments")
+        self.nseg, self.ncomb, self.npart = nseg.value, ncomb.value, npart.value
+        self.segments = self.segments[:self.nseg]
+        self.combines = self.combines[:self.ncomb]
+        self.d_seg = self.d_comb = self.d_work = None
+
+    def to(self, device):
+        import torch
+        self.d_seg = torch.from_numpy(self.segments.view(np.uint8).copy()).to(device)
+        self.d_comb = torch.from_numpy(self.combines.view(np.uint8).copy()).to(device)
+        self.d_work = torch.empty(max(self.npart, 1) * 64, dtype=torch.uint8, device=device)
+        return self
+
+
+def seal_segments(desc, plan, inp, out, subkeys_t, stream=None, desc_np=None):
+    """Ragged seal with long frames split across lanes (same output as seal_batch)."""
+    _need_cuda_u8(inp, "in")
+    _need_cuda_u8(out, "out")
+    if desc_np is not None:
+        _check_desc_bounds(desc_np, inp.numel(), out.numel(), subkeys_t.shape[0], True)
+    _lib.check(_lib.lib().cz_seal_segments(_ptr(desc), _ptr(plan.d_seg), plan.nseg, _ptr(plan.d_comb), plan.ncomb,
+                                           _ptr(inp), _ptr(out), _ptr(subkeys_t), _ptr(plan.d_work),
+                                           _stream(stream)), "cz_seal_segments")
+
+
+def open_segments(desc, plan, inp, out, subkeys_t, status, nonces=None, stream=None, desc_np=None):
+    """Ragged open with long frames split across lanes (same output as open_batch)."""
+    _need_cuda_u8(inp, "in")
+    _need_cuda_u8(out, "out")
+    if desc_np is not None:
+        _check_desc_bounds(desc_np, inp.numel(), out.numel(), subkeys_t.shape[0], False)
+    _lib.check(_lib.lib().cz_open_segments(_ptr(desc), _ptr(plan.d_seg), plan.nseg, _ptr(plan.d_comb), plan.ncomb,
+                                           _ptr(inp), _ptr(out), _ptr(subkeys_t), _ptr(plan.d_work), _ptr(status),
+                                           _ptr(nonces), _stream(stream)), "cz_open_segments")

@@ -181,6 +181,97 @@ __device__ __forceinline__ void poly_finish(const Poly &P, u32 tag[4])
     t = (u64)h3 + P.p3 + (t >> 32); tag[3] = (u32)t;
 }
 
+// ---- general arithmetic mod p = 2^130 - 5, radix 2^26 -----------------------
+// Used to combine the Poly1305 partials of a frame split into segments: the
+// frame's accumulator is H = sum_s h_s * r^(m_{s+1} + ... + m_{S-1}), evaluated
+// as a Horner chain over segments with multipliers r^m.  r^m is not clamped, so
+// the 2^32-radix 5/4 trick does not apply; 26-bit limbs with 5*b_j < 2^29 do.
+struct F26 {
+    u32 l[5];
+};
+
+// from 32-bit limbs h0..h3 + small h4 (h < 2^131)
+__device__ __forceinline__ F26 f26_from32(u32 h0, u32 h1, u32 h2, u32 h3, u32 h4)
+{
+    F26 a;
+    a.l[0] = h0 & 0x3ffffffu;
+    a.l[1] = ((h0 >> 26) | (h1 << 6)) & 0x3ffffffu;
+    a.l[2] = ((h1 >> 20) | (h2 << 12)) & 0x3ffffffu;
+    a.l[3] = ((h2 >> 14) | (h3 << 18)) & 0x3ffffffu;
+    a.l[4] = (h3 >> 8) | (h4 << 24);
+    return a;
+}
+
+// a * b mod p (partially reduced: limbs < 2^26 except l[1] < 2^26 + 2^6); inputs' limbs < 2^27
+__device__ __forceinline__ F26 f26_mul(const F26 &a, const F26 &b)
+{
+    const u32 s1 = b.l[1] * 5u, s2 = b.l[2] * 5u, s3 = b.l[3] * 5u, s4 = b.l[4] * 5u;
+    u64 d0 = (u64)a.l[0] * b.l[0] + (u64)a.l[1] * s4 + (u64)a.l[2] * s3 + (u64)a.l[3] * s2 + (u64)a.l[4] * s1;
+    u64 d1 = (u64)a.l[0] * b.l[1] + (u64)a.l[1] * b.l[0] + (u64)a.l[2] * s4 + (u64)a.l[3] * s3 + (u64)a.l[4] * s2;
+    u64 d2 = (u64)a.l[0] * b.l[2] + (u64)a.l[1] * b.l[1] + (u64)a.l[2] * b.l[0] + (u64)a.l[3] * s4 + (u64)a.l[4] * s3;
+    u64 d3 = (u64)a.l[0] * b.l[3] + (u64)a.l[1] * b.l[2] + (u64)a.l[2] * b.l[1] + (u64)a.l[3] * b.l[0] + (u64)a.l[4] * s4;
+    u64 d4 = (u64)a.l[0] * b.l[4] + (u64)a.l[1] * b.l[3] + (u64)a.l[2] * b.l[2] + (u64)a.l[3] * b.l[1] + (u64)a.l[4] * b.l[0];
+    F26 r;
+    d1 += d0 >> 26; r.l[0] = (u32)d0 & 0x3ffffffu;
+    d2 += d1 >> 26; r.l[1] = (u32)d1 & 0x3ffffffu;
+    d3 += d2 >> 26; r.l[2] = (u32)d2 & 0x3ffffffu;
+    d4 += d3 >> 26; r.l[3] = (u32)d3 & 0x3ffffffu;
+    u64 c = d4 >> 26; r.l[4] = (u32)d4 & 0x3ffffffu;
+    u64 t = (u64)r.l[0] + c * 5u;
+    r.l[0] = (u32)t & 0x3ffffffu;
+    r.l[1] += (u32)(t >> 26);
+    return r;
+}
+
+__device__ __forceinline__ F26 f26_add(const F26 &a, const F26 &b)
+{
+    F26 r;
+    u32 c = 0;
+#pragma unroll
+    for (int i = 0; i < 5; i++) {
+        u32 v = a.l[i] + b.l[i] + c;
+        r.l[i] = v & 0x3ffffffu;
+        c = v >> 26;
+    }
+    u32 t = r.l[0] + c * 5u;
+    r.l[0] = t & 0x3ffffffu;
+    r.l[1] += t >> 26;
+    return r;
+}
+
+// r^e for e >= 1 (square and multiply)
+__device__ __forceinline__ F26 f26_pow(const F26 &r, u32 e)
+{
+    F26 acc = r, base = r;
+    bool have = false;
+    for (u32 bit = 0; e >> bit; bit++) {
+        if (bit)
+            base = f26_mul(base, base);
+        if ((e >> bit) & 1u) {
+            acc = have ? f26_mul(acc, base) : base;
+            have = true;
+        }
+    }
+    return acc;
+}
+
+// back to 32-bit limbs h0..h3 + small h4 (input for poly_finish)
+__device__ __forceinline__ void f26_to32(const F26 &a, u32 &h0, u32 &h1, u32 &h2, u32 &h3, u32 &h4)
+{
+    u32 l0 = a.l[0], l1 = a.l[1], l2 = a.l[2], l3 = a.l[3], l4 = a.l[4], c;
+    c = l1 >> 26; l1 &= 0x3ffffffu;
+    l2 += c; c = l2 >> 26; l2 &= 0x3ffffffu;
+    l3 += c; c = l3 >> 26; l3 &= 0x3ffffffu;
+    l4 += c; c = l4 >> 26; l4 &= 0x3ffffffu;
+    l0 += c * 5u; c = l0 >> 26; l0 &= 0x3ffffffu;
+    l1 += c;
+    h0 = l0 | (l1 << 26);
+    h1 = (l1 >> 6) | (l2 << 20);
+    h2 = (l2 >> 12) | (l3 << 14);
+    h3 = (l3 >> 18) | (l4 << 8);
+    h4 = l4 >> 24;
+}
+
 __device__ __forceinline__ u32 bswap32(u32 v) { return __builtin_bswap32(v); }
 
 // Salsa20 nonce words for a CurveZMQ MESSAGE counter: the nonce tail is

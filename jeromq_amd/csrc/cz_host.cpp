@@ -28,6 +28,10 @@ hipError_t czk_box_nacl(const void *, void *, uint32_t, const void *, uint64_t, 
 hipError_t czk_subkeys(const void *, void *, uint32_t, const uint8_t *, hipStream_t);
 hipError_t czk_fill(void *, uint64_t, uint64_t, hipStream_t);
 int czk_tune(const char *, int);
+hipError_t czk_seal_segments(const cz_frame_desc *, const cz_segment *, uint32_t, const cz_combine *, uint32_t,
+                             const void *, void *, const void *, void *, hipStream_t);
+hipError_t czk_open_segments(const cz_frame_desc *, const cz_segment *, uint32_t, const cz_combine *, uint32_t,
+                             const void *, void *, const void *, void *, uint16_t *, uint64_t *, hipStream_t);
 }
 
 namespace czi {
@@ -319,6 +323,73 @@ int cz_plan_order(const cz_frame_desc *h_desc, uint32_t count, uint32_t *h_order
     std::stable_sort(h_order, h_order + count,
                      [h_desc](uint32_t a, uint32_t b) { return h_desc[a].len > h_desc[b].len; });
     return CZ_OK;
+}
+
+int cz_plan_segments(const cz_frame_desc *h_desc, uint32_t count, int open, uint32_t seg_blocks, cz_segment *h_seg,
+                     uint32_t seg_cap, uint32_t *nseg, cz_combine *h_comb, uint32_t comb_cap, uint32_t *ncomb,
+                     uint32_t *npart)
+{
+    if ((count && !h_desc) || !nseg || !ncomb || !npart)
+        return fail(CZ_EINVAL, "cz_plan_segments: null pointer");
+    if (seg_blocks < 2)
+        return fail(CZ_EINVAL, "cz_plan_segments: seg_blocks must be >= 2");
+    const uint32_t split_above = seg_blocks + seg_blocks / 2;
+    std::vector<cz_segment> segs;
+    std::vector<cz_combine> combs;
+    segs.reserve(count);
+    uint32_t parts = 0;
+    for (uint32_t i = 0; i < count; i++) {
+        const uint64_t mlen = open ? (uint64_t)h_desc[i].len : (uint64_t)h_desc[i].len + CZ_MESSAGE_OVERHEAD;
+        uint32_t nblk = (uint32_t)((mlen + 63) / 64);
+        if (nblk == 0)
+            nblk = 1;
+        if (nblk <= split_above) {
+            segs.push_back({i, 0u, nblk, 0xffffffffu});
+            continue;
+        }
+        const uint32_t ns = (nblk + seg_blocks - 1) / seg_blocks;  // last segment takes the remainder
+        combs.push_back({i, parts, ns, 0u});
+        for (uint32_t s = 0; s < ns; s++)
+            segs.push_back({i, s * seg_blocks, s + 1 < ns ? seg_blocks : nblk - s * seg_blocks, parts + s});
+        parts += ns;
+    }
+    std::stable_sort(segs.begin(), segs.end(),
+                     [](const cz_segment &a, const cz_segment &b) { return a.nblocks > b.nblocks; });
+    *nseg = (uint32_t)segs.size();
+    *ncomb = (uint32_t)combs.size();
+    *npart = parts;
+    if (segs.size() > seg_cap || combs.size() > comb_cap || (segs.size() && !h_seg) || (combs.size() && !h_comb))
+        return fail(CZ_EINVAL, "cz_plan_segments: capacity too small (need %u segments, %u combines)", *nseg,
+                    *ncomb);
+    std::copy(segs.begin(), segs.end(), h_seg);
+    std::copy(combs.begin(), combs.end(), h_comb);
+    return CZ_OK;
+}
+
+int cz_seal_segments(const cz_frame_desc *d_desc, const cz_segment *d_seg, uint32_t nseg, const cz_combine *d_comb,
+                     uint32_t ncomb, const void *d_in, void *d_out, const void *d_subkeys, void *d_work,
+                     void *stream)
+{
+    if (nseg && (!d_desc || !d_seg || !d_in || !d_out || !d_subkeys))
+        return fail(CZ_EINVAL, "cz_seal_segments: null pointer");
+    if (ncomb && (!d_comb || !d_work))
+        return fail(CZ_EINVAL, "cz_seal_segments: null combine list / workspace");
+    hipError_t e = czk_seal_segments(d_desc, d_seg, nseg, d_comb, ncomb, d_in, d_out, d_subkeys, d_work,
+                                     (hipStream_t)stream);
+    return e == hipSuccess ? CZ_OK : hip_fail(e, "cz_seal_segments");
+}
+
+int cz_open_segments(const cz_frame_desc *d_desc, const cz_segment *d_seg, uint32_t nseg, const cz_combine *d_comb,
+                     uint32_t ncomb, const void *d_in, void *d_out, const void *d_subkeys, void *d_work,
+                     uint16_t *d_status, uint64_t *d_nonces, void *stream)
+{
+    if (nseg && (!d_desc || !d_seg || !d_in || !d_out || !d_subkeys || !d_status))
+        return fail(CZ_EINVAL, "cz_open_segments: null pointer");
+    if (ncomb && (!d_comb || !d_work))
+        return fail(CZ_EINVAL, "cz_open_segments: null combine list / workspace");
+    hipError_t e = czk_open_segments(d_desc, d_seg, nseg, d_comb, ncomb, d_in, d_out, d_subkeys, d_work, d_status,
+                                     d_nonces, (hipStream_t)stream);
+    return e == hipSuccess ? CZ_OK : hip_fail(e, "cz_open_segments");
 }
 
 int cz_fill(void *d_buf, uint64_t nbytes, uint64_t seed, void *stream)

@@ -798,6 +798,300 @@ __device__ __forceinline__ u64 read_be64(const uint8_t *p)
     return v;
 }
 
+// ---------------------------------------------------------------------------
+// Segmented frames (ragged batches).  A frame longer than 1.5 x SEG blocks is
+// split into SEG-block segments, one per lane, so a 64 KiB frame no longer pins
+// one lane for 1025 sequential blocks (the Zipf batch's critical path).  A
+// segment lane runs Poly1305 from h = 0 over its own blocks and writes a
+// 64-byte partial record; k_*_combine joins a frame's records with r^m powers.
+// Record: [0..4] h (2^32 radix, partially reduced), [5] poly blocks absorbed,
+// [6] decrypted flags byte (open, segment 0), [7] early status (open, segment 0),
+// [8..11] clamped r, [12..15] pad (segment 0).
+// ---------------------------------------------------------------------------
+template <bool AL>
+__device__ __forceinline__ u32 ld32(const uint8_t *__restrict__ p)
+{
+    if constexpr (AL)
+        return *reinterpret_cast<const u32 *>(p);
+    else
+        return (u32)p[0] | ((u32)p[1] << 8) | ((u32)p[2] << 16) | ((u32)p[3] << 24);
+}
+
+template <bool AL>
+__device__ void seal_segment(const uint8_t *__restrict__ in, uint8_t *__restrict__ out, u32 n, u32 flags,
+                             u64 counter, const u32 key[8], u32 b0, u32 b1, u32 *__restrict__ rec)
+{
+    const u32 mlen = n + 33u;
+    const u32 nblk = (mlen + 63u) >> 6;
+    const u32 nfull = mlen >> 6;
+    const u32 tailv = mlen & 63u;
+    const u32 bend = b1 < nblk ? b1 : nblk;
+    const u64 inlen = n;
+    u32 n0, n1;
+    counter_nonce(counter, n0, n1);
+    u32 x[16], C[16];
+    salsa20_block(x, key, n0, n1, 0u, 0u);
+    Poly P;
+    poly_init(P, x[0], x[1], x[2], x[3], x[4], x[5], x[6], x[7]);
+    EmitDirect<AL> em{out, mlen};
+    u32 carry, blk, mpoly = 0;
+    if (b0 == 0) {
+        V4 a = ld16<AL>(in, inlen);
+        V4 b = ld16<AL>(in + 16, inlen > 16 ? inlen - 16 : 0);
+        u32 W[9] = {flags << 24, a.x, a.y, a.z, a.w, b.x, b.y, b.z, b.w};
+#pragma unroll
+        for (int k = 8; k < 16; k++)
+            C[k] = funnel(W[k - 7], W[k - 8], 3) ^ x[k];
+        carry = b.w;
+        C[0] = HDR0; C[1] = HDR1; C[2] = n0; C[3] = n1;
+        C[4] = C[5] = C[6] = C[7] = 0u;
+        if (nfull >= 1) {
+            poly_block(P, C[8], C[9], C[10], C[11], 1u);
+            poly_block(P, C[12], C[13], C[14], C[15], 1u);
+            mpoly = 2;
+        } else {
+            u32 nb = mlen - 32u;
+            if (nb >= 16u) {
+                poly_block(P, C[8], C[9], C[10], C[11], 1u);
+                if (nb > 16u)
+                    poly_block_partial(P, C[12], C[13], C[14], C[15], nb - 16u);
+            } else {
+                poly_block_partial(P, C[8], C[9], C[10], C[11], nb);
+            }
+            mpoly = (nb + 15u) >> 4;
+        }
+        em.emit(0, C);
+        blk = 1;
+    } else {
+        carry = ld32<AL>(in + 64u * b0 - 36u);  // payload dword P[16*b0 - 9]
+        blk = b0;
+    }
+    const u32 fend = nfull < bend ? nfull : bend;
+    for (; blk < fend; blk++) {
+        const uint8_t *src = in + 64u * blk - 32u;
+        V4 q0 = ld16f<AL>(src), q1 = ld16f<AL>(src + 16), q2 = ld16f<AL>(src + 32);
+        V4 q3 = ld16<AL>(src + 48, inlen - (64u * blk + 16u));
+        u32 W[17] = {carry, q0.x, q0.y, q0.z, q0.w, q1.x, q1.y, q1.z, q1.w,
+                     q2.x, q2.y, q2.z, q2.w, q3.x, q3.y, q3.z, q3.w};
+        salsa20_block(x, key, n0, n1, blk, 0u);
+#pragma unroll
+        for (int k = 0; k < 16; k++)
+            C[k] = funnel(W[k + 1], W[k], 3) ^ x[k];
+        carry = q3.w;
+        poly_block(P, C[0], C[1], C[2], C[3], 1u);
+        poly_block(P, C[4], C[5], C[6], C[7], 1u);
+        poly_block(P, C[8], C[9], C[10], C[11], 1u);
+        poly_block(P, C[12], C[13], C[14], C[15], 1u);
+        mpoly += 4;
+        em.emit(blk, C);
+    }
+    if (tailv != 0 && nfull >= 1 && nfull < bend) {
+        const u32 tb = nfull;
+        V4 q[4];
+#pragma unroll
+        for (int c = 0; c < 4; c++) {
+            long o = (long)(64u * tb) - 32 + 16 * c;
+            u64 avail = (o >= 0 && (u64)o < inlen) ? inlen - (u64)o : 0;
+            q[c] = ld16<AL>(in + o, avail);
+        }
+        salsa20_block(x, key, n0, n1, tb, 0u);
+        u32 W[17] = {carry, q[0].x, q[0].y, q[0].z, q[0].w, q[1].x, q[1].y, q[1].z, q[1].w,
+                     q[2].x, q[2].y, q[2].z, q[2].w, q[3].x, q[3].y, q[3].z, q[3].w};
+#pragma unroll
+        for (int k = 0; k < 16; k++)
+            C[k] = funnel(W[k + 1], W[k], 3) ^ x[k];
+#pragma unroll
+        for (int j = 0; j < 4; j++) {
+            u32 s = 16u * j;
+            if (s < tailv) {
+                u32 nb = tailv - s;
+                if (nb >= 16)
+                    poly_block(P, C[4 * j], C[4 * j + 1], C[4 * j + 2], C[4 * j + 3], 1u);
+                else
+                    poly_block_partial(P, C[4 * j], C[4 * j + 1], C[4 * j + 2], C[4 * j + 3], nb);
+            }
+        }
+        mpoly += (tailv + 15u) >> 4;
+        em.emit(tb, C);
+    }
+    if (!rec) {
+        u32 tag[4];
+        poly_finish(P, tag);
+        em.tag(tag);
+        return;
+    }
+    rec[0] = P.h0; rec[1] = P.h1; rec[2] = P.h2; rec[3] = P.h3; rec[4] = P.h4; rec[5] = mpoly;
+    if (b0 == 0) {
+        rec[8] = P.r0; rec[9] = P.r1; rec[10] = P.r2; rec[11] = P.r3;
+        rec[12] = P.p0; rec[13] = P.p1; rec[14] = P.p2; rec[15] = P.p3;
+    }
+}
+
+// Open one segment [b0, b1) of a MESSAGE body.  Emits payload chunks
+// [b0-1, b1-1) (the 33-byte shift lags the payload one block behind the body),
+// so a segment with b0 > 0 first recomputes block b0-1's plaintext tail.
+template <bool AL>
+__device__ u32 open_segment(const uint8_t *__restrict__ in, uint8_t *__restrict__ out, u32 size, const u32 key[8],
+                            bool check_floor, long long floor, u32 *flags_out, u64 *nonce_out, u32 b0, u32 b1,
+                            u32 *__restrict__ rec)
+{
+    V4 h = ld16<AL>(in, size);
+    if (size < 8u || h.x != HDR0 || (h.y & 0x00ffffffu) != (HDR1 & 0x00ffffffu))
+        return CZ_STATUS_COMMAND;
+    if (size < 33u)
+        return CZ_STATUS_MALFORMED;
+    const u32 n0 = h.z, n1 = h.w;
+    const u64 nonce = ((u64)bswap32(n0) << 32) | (u64)bswap32(n1);
+    *nonce_out = nonce;
+    if (check_floor && (long long)nonce <= floor)
+        return CZ_STATUS_SEQUENCE;
+
+    const u32 mlen = size;
+    const u32 nblk = (mlen + 63u) >> 6;
+    const u32 nfull = mlen >> 6;
+    const u32 nout = size - 33u;
+    const u32 bend = b1 < nblk ? b1 : nblk;
+    u32 x[16], C[16], X[16], K[8];
+    salsa20_block(x, key, n0, n1, 0u, 0u);
+    Poly P;
+    poly_init(P, x[0], x[1], x[2], x[3], x[4], x[5], x[6], x[7]);
+    EmitDirect<AL> em{out, nout};
+    u32 blk, mpoly = 0;
+    if (b0 == 0) {
+        V4 a = ld16<AL>(in + 32, size > 32 ? size - 32u : 0);
+        V4 b = ld16<AL>(in + 48, size > 48 ? size - 48u : 0);
+        C[8] = a.x; C[9] = a.y; C[10] = a.z; C[11] = a.w;
+        C[12] = b.x; C[13] = b.y; C[14] = b.z; C[15] = b.w;
+        if (nfull >= 1) {
+            poly_block(P, C[8], C[9], C[10], C[11], 1u);
+            poly_block(P, C[12], C[13], C[14], C[15], 1u);
+            mpoly = 2;
+        } else {
+            u32 nb = mlen - 32u;
+            if (nb >= 16u) {
+                poly_block(P, C[8], C[9], C[10], C[11], 1u);
+                if (nb > 16u)
+                    poly_block_partial(P, C[12], C[13], C[14], C[15], nb - 16u);
+            } else {
+                poly_block_partial(P, C[8], C[9], C[10], C[11], nb);
+            }
+            mpoly = (nb + 15u) >> 4;
+        }
+#pragma unroll
+        for (int k = 0; k < 8; k++)
+            K[k] = C[8 + k] ^ x[8 + k];
+        *flags_out = K[0] & 0xffu;
+        blk = 1;
+    } else {
+        // plaintext dwords 8..15 of block b0-1 (its MAC belongs to the previous segment)
+        salsa20_block(X, key, n0, n1, b0 - 1u, 0u);
+        const uint8_t *src = in + 64u * (b0 - 1u) + 32u;
+        V4 a = ld16f<AL>(src), b = ld16f<AL>(src + 16);
+        K[0] = a.x ^ X[8]; K[1] = a.y ^ X[9]; K[2] = a.z ^ X[10]; K[3] = a.w ^ X[11];
+        K[4] = b.x ^ X[12]; K[5] = b.y ^ X[13]; K[6] = b.z ^ X[14]; K[7] = b.w ^ X[15];
+        blk = b0;
+    }
+    for (; blk < bend; blk++) {
+        const uint8_t *src = in + 64u * blk;
+        const bool full = blk < nfull;
+        V4 q0, q1, q2, q3;
+        if (full) {
+            q0 = ld16f<AL>(src); q1 = ld16f<AL>(src + 16); q2 = ld16f<AL>(src + 32); q3 = ld16f<AL>(src + 48);
+        } else {
+            const u32 o = 64u * blk;
+            q0 = ld16<AL>(src, size - o);
+            q1 = ld16<AL>(src + 16, o + 16u < size ? size - o - 16u : 0);
+            q2 = ld16<AL>(src + 32, o + 32u < size ? size - o - 32u : 0);
+            q3 = ld16<AL>(src + 48, o + 48u < size ? size - o - 48u : 0);
+        }
+        C[0] = q0.x; C[1] = q0.y; C[2] = q0.z; C[3] = q0.w;
+        C[4] = q1.x; C[5] = q1.y; C[6] = q1.z; C[7] = q1.w;
+        C[8] = q2.x; C[9] = q2.y; C[10] = q2.z; C[11] = q2.w;
+        C[12] = q3.x; C[13] = q3.y; C[14] = q3.z; C[15] = q3.w;
+        salsa20_block(x, key, n0, n1, blk, 0u);
+        if (full) {
+            poly_block(P, C[0], C[1], C[2], C[3], 1u);
+            poly_block(P, C[4], C[5], C[6], C[7], 1u);
+            poly_block(P, C[8], C[9], C[10], C[11], 1u);
+            poly_block(P, C[12], C[13], C[14], C[15], 1u);
+            mpoly += 4;
+        } else {
+            const u32 tailv = mlen - 64u * blk;
+#pragma unroll
+            for (int j = 0; j < 4; j++) {
+                u32 s = 16u * j;
+                if (s < tailv) {
+                    u32 nb = tailv - s;
+                    if (nb >= 16)
+                        poly_block(P, C[4 * j], C[4 * j + 1], C[4 * j + 2], C[4 * j + 3], 1u);
+                    else
+                        poly_block_partial(P, C[4 * j], C[4 * j + 1], C[4 * j + 2], C[4 * j + 3], nb);
+                }
+            }
+            mpoly += (tailv + 15u) >> 4;
+        }
+#pragma unroll
+        for (int k = 0; k < 16; k++)
+            X[k] = C[k] ^ x[k];
+        u32 O[16];
+        u32 E[17] = {K[0], K[1], K[2], K[3], K[4], K[5], K[6], K[7], X[0], X[1], X[2], X[3], X[4], X[5], X[6], X[7],
+                     X[8]};
+#pragma unroll
+        for (int t = 0; t < 16; t++)
+            O[t] = funnel(E[t + 1], E[t], 1);
+        em.emit(blk - 1u, O);
+#pragma unroll
+        for (int k = 0; k < 8; k++)
+            K[k] = X[8 + k];
+    }
+    if (bend == nblk && 64u * (nblk - 1u) < nout) {
+        u32 O[16];
+#pragma unroll
+        for (int t = 0; t < 16; t++)
+            O[t] = t < 7 ? funnel(K[t + 1], K[t], 1) : (t == 7 ? funnel(0u, K[7], 1) : 0u);
+        em.emit(nblk - 1u, O);
+    }
+    if (!rec) {
+        u32 tag[4];
+        poly_finish(P, tag);
+        V4 tin = ld16<AL>(in + 16, size - 16u);
+        if ((tag[0] ^ tin.x) | (tag[1] ^ tin.y) | (tag[2] ^ tin.z) | (tag[3] ^ tin.w)) {
+            em.poison();
+            return CZ_STATUS_CRYPTO;
+        }
+        return CZ_STATUS_OK;
+    }
+    rec[0] = P.h0; rec[1] = P.h1; rec[2] = P.h2; rec[3] = P.h3; rec[4] = P.h4; rec[5] = mpoly;
+    if (b0 == 0) {
+        rec[6] = *flags_out;
+        rec[8] = P.r0; rec[9] = P.r1; rec[10] = P.r2; rec[11] = P.r3;
+        rec[12] = P.p0; rec[13] = P.p1; rec[14] = P.p2; rec[15] = P.p3;
+    }
+    return CZ_STATUS_OK;
+}
+
+// Join a frame's segment records: H = Horner over segments with multipliers r^m.
+__device__ __forceinline__ void combine_tag(const u32 *__restrict__ R0, u32 nseg, u32 tag[4])
+{
+    const F26 r = f26_from32(R0[8], R0[9], R0[10], R0[11], 0u);
+    F26 H = f26_from32(R0[0], R0[1], R0[2], R0[3], R0[4]);
+    u32 cached_m = 0;
+    F26 cached;
+    for (u32 s = 1; s < nseg; s++) {
+        const u32 *R = R0 + 16u * s;
+        const u32 m = R[5];
+        if (m != cached_m) {
+            cached = f26_pow(r, m);
+            cached_m = m;
+        }
+        H = f26_add(f26_mul(H, cached), f26_from32(R[0], R[1], R[2], R[3], R[4]));
+    }
+    Poly Q;
+    f26_to32(H, Q.h0, Q.h1, Q.h2, Q.h3, Q.h4);
+    Q.p0 = R0[12]; Q.p1 = R0[13]; Q.p2 = R0[14]; Q.p3 = R0[15];
+    poly_finish(Q, tag);
+}
+
 // ---- kernels -------------------------------------------------------------
 
 enum Staging { ST_DIRECT = 0, ST_LINES = 1, ST_REGION = 2 };
@@ -983,6 +1277,124 @@ __global__ __launch_bounds__(BLOCK) void k_open_uniform(const uint8_t *__restric
         st = open_frame<MODE_ZMQ, false>(src, size, key, check != 0, floor, &fl, &nonce, 0, em);
     }
     status[i] = (uint16_t)(st | (st == CZ_STATUS_OK ? (fl << 8) : 0u));
+}
+
+
+// ---- segmented (ragged) batches ------------------------------------------
+__global__ __launch_bounds__(BLOCK) void k_seal_segments(const cz_frame_desc *__restrict__ desc,
+                                                          const cz_segment *__restrict__ segs, uint32_t nseg,
+                                                          const uint8_t *__restrict__ in, uint8_t *__restrict__ out,
+                                                          const uint8_t *__restrict__ subkeys,
+                                                          u32 *__restrict__ work)
+{
+    const uint32_t t = blockIdx.x * BLOCK + threadIdx.x;
+    if (t >= nseg)
+        return;
+    const cz_segment sg = segs[t];
+    const cz_frame_desc d = desc[sg.frame];
+    u32 key[8];
+    load_key(subkeys + 32ull * d.key_idx, key);
+    u32 *rec = sg.part == 0xffffffffu ? nullptr : work + 16ull * sg.part;
+    const uint8_t *src = in + d.in_off;
+    uint8_t *dst = out + d.out_off;
+    const u32 b1 = sg.first_block + sg.nblocks;
+    if (aligned16(src, dst))
+        seal_segment<true>(src, dst, d.len, d.flags & 0xffu, d.counter, key, sg.first_block, b1, rec);
+    else
+        seal_segment<false>(src, dst, d.len, d.flags & 0xffu, d.counter, key, sg.first_block, b1, rec);
+}
+
+__global__ __launch_bounds__(BLOCK) void k_seal_combine(const cz_frame_desc *__restrict__ desc,
+                                                         const cz_combine *__restrict__ comb, uint32_t ncomb,
+                                                         uint8_t *__restrict__ out, const u32 *__restrict__ work)
+{
+    const uint32_t t = blockIdx.x * BLOCK + threadIdx.x;
+    if (t >= ncomb)
+        return;
+    const cz_combine cb = comb[t];
+    const cz_frame_desc d = desc[cb.frame];
+    u32 tag[4];
+    combine_tag(work + 16ull * cb.part0, cb.nseg, tag);
+    uint8_t *dst = out + d.out_off + 16;
+    if ((((uintptr_t)dst) & 15u) == 0)
+        st16<true>(dst, tag[0], tag[1], tag[2], tag[3]);
+    else
+        st16<false>(dst, tag[0], tag[1], tag[2], tag[3]);
+}
+
+__global__ __launch_bounds__(BLOCK) void k_open_segments(const cz_frame_desc *__restrict__ desc,
+                                                          const cz_segment *__restrict__ segs, uint32_t nseg,
+                                                          const uint8_t *__restrict__ in, uint8_t *__restrict__ out,
+                                                          const uint8_t *__restrict__ subkeys,
+                                                          u32 *__restrict__ work, uint16_t *__restrict__ status,
+                                                          uint64_t *__restrict__ nonces)
+{
+    const uint32_t t = blockIdx.x * BLOCK + threadIdx.x;
+    if (t >= nseg)
+        return;
+    const cz_segment sg = segs[t];
+    const cz_frame_desc d = desc[sg.frame];
+    u32 key[8];
+    load_key(subkeys + 32ull * d.key_idx, key);
+    long long floor = (long long)d.counter;
+    if (d.prev >= 0)
+        floor = (long long)read_be64(in + desc[d.prev].in_off + 8);
+    const bool check = (d.flags & CZ_DESC_CHECK_NONCE) != 0;
+    const uint8_t *src = in + d.in_off;
+    uint8_t *dst = out + d.out_off;
+    u32 *rec = sg.part == 0xffffffffu ? nullptr : work + 16ull * sg.part;
+    u32 fl = 0;
+    u64 nonce = 0;
+    const u32 b1 = sg.first_block + sg.nblocks;
+    u32 st;
+    if (aligned16(src, dst))
+        st = open_segment<true>(src, dst, d.len, key, check, floor, &fl, &nonce, sg.first_block, b1, rec);
+    else
+        st = open_segment<false>(src, dst, d.len, key, check, floor, &fl, &nonce, sg.first_block, b1, rec);
+    if (sg.first_block == 0) {
+        if (nonces)
+            nonces[sg.frame] = nonce;
+        if (!rec)
+            status[sg.frame] = (uint16_t)(st | (st == CZ_STATUS_OK ? (fl << 8) : 0u));
+        else {
+            rec[7] = st;  // early rejects are final; the combine kernel finishes OK frames
+            if (st != CZ_STATUS_OK)
+                status[sg.frame] = (uint16_t)st;
+        }
+    }
+}
+
+__global__ __launch_bounds__(BLOCK) void k_open_combine(const cz_frame_desc *__restrict__ desc,
+                                                         const cz_combine *__restrict__ comb, uint32_t ncomb,
+                                                         const uint8_t *__restrict__ in, uint8_t *__restrict__ out,
+                                                         const u32 *__restrict__ work,
+                                                         uint16_t *__restrict__ status)
+{
+    const uint32_t t = blockIdx.x * BLOCK + threadIdx.x;
+    if (t >= ncomb)
+        return;
+    const cz_combine cb = comb[t];
+    const u32 *R0 = work + 16ull * cb.part0;
+    if (R0[7] != CZ_STATUS_OK)
+        return;
+    const cz_frame_desc d = desc[cb.frame];
+    u32 tag[4];
+    combine_tag(R0, cb.nseg, tag);
+    const uint8_t *tp = in + d.in_off + 16;
+    u32 tin[4];
+    for (int w = 0; w < 4; w++)
+        tin[w] = (u32)tp[4 * w] | ((u32)tp[4 * w + 1] << 8) | ((u32)tp[4 * w + 2] << 16) |
+                 ((u32)tp[4 * w + 3] << 24);
+    if ((tag[0] ^ tin[0]) | (tag[1] ^ tin[1]) | (tag[2] ^ tin[2]) | (tag[3] ^ tin[3])) {
+        // never release unauthenticated plaintext: zero what the segments wrote
+        uint8_t *dst = out + d.out_off;
+        const u32 nout = d.len - 33u;
+        for (u32 o = 0; o < nout; o++)
+            dst[o] = 0;
+        status[cb.frame] = CZ_STATUS_CRYPTO;
+    } else {
+        status[cb.frame] = (uint16_t)(CZ_STATUS_OK | (R0[6] << 8));
+    }
 }
 
 // NaCl-layout single frame (jnacl crypto_box_afternm / crypto_box_open_afternm drop-in).
@@ -1184,6 +1596,31 @@ hipError_t czk_subkeys(const void *precom, void *out, uint32_t nkeys, const uint
     dim3 grid((nkeys + BLOCK - 1) / BLOCK);
     hipLaunchKernelGGL(k_subkeys, grid, dim3(BLOCK), 0, s, (const uint8_t *)precom, (uint8_t *)out, nkeys, p[0], p[1],
                        p[2], p[3]);
+    return hipGetLastError();
+}
+
+hipError_t czk_seal_segments(const cz_frame_desc *desc, const cz_segment *segs, uint32_t nseg, const cz_combine *comb,
+                             uint32_t ncomb, const void *in, void *out, const void *subkeys, void *work, hipStream_t s)
+{
+    if (nseg)
+        hipLaunchKernelGGL(k_seal_segments, dim3((nseg + BLOCK - 1) / BLOCK), dim3(BLOCK), 0, s, desc, segs, nseg,
+                           (const uint8_t *)in, (uint8_t *)out, (const uint8_t *)subkeys, (u32 *)work);
+    if (ncomb)
+        hipLaunchKernelGGL(k_seal_combine, dim3((ncomb + BLOCK - 1) / BLOCK), dim3(BLOCK), 0, s, desc, comb, ncomb,
+                           (uint8_t *)out, (const u32 *)work);
+    return hipGetLastError();
+}
+
+hipError_t czk_open_segments(const cz_frame_desc *desc, const cz_segment *segs, uint32_t nseg, const cz_combine *comb,
+                             uint32_t ncomb, const void *in, void *out, const void *subkeys, void *work,
+                             uint16_t *status, uint64_t *nonces, hipStream_t s)
+{
+    if (nseg)
+        hipLaunchKernelGGL(k_open_segments, dim3((nseg + BLOCK - 1) / BLOCK), dim3(BLOCK), 0, s, desc, segs, nseg,
+                           (const uint8_t *)in, (uint8_t *)out, (const uint8_t *)subkeys, (u32 *)work, status, nonces);
+    if (ncomb)
+        hipLaunchKernelGGL(k_open_combine, dim3((ncomb + BLOCK - 1) / BLOCK), dim3(BLOCK), 0, s, desc, comb, ncomb,
+                           (const uint8_t *)in, (uint8_t *)out, (const u32 *)work, status);
     return hipGetLastError();
 }
 

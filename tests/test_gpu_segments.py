@@ -1,0 +1,189 @@
+"""GPU parity for segmented ragged batches (cz_seal_segments / cz_open_segments).
+
+Long frames are split across lanes and their Poly1305 partials joined by the
+combine kernels; the output contract is cz_seal_batch's / cz_open_batch's, so
+every case is checked bit-exact against the CPU oracle (seal: or_seal_batch;
+open: or_curve_decode semantics via the golden statuses) and against the
+one-lane-per-frame kernels.  Small seg_blocks values put segment boundaries
+inside short frames, so every boundary/tail position is reached cheaply.
+"""
+import numpy as np
+import pytest
+
+from cz_testlib import DESC_DTYPE, load_golden, oracle, or_curve_encode, splitmix_bytes
+
+pytestmark = pytest.mark.gpu
+
+G = load_golden()
+PRECOM = bytes.fromhex(G["keys"]["precom"])
+
+
+@pytest.fixture(scope="module")
+def torch_dev():
+    import torch
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    return torch, torch.device("cuda:0")
+
+
+@pytest.fixture(scope="module")
+def L():
+    from jeromq_amd import _lib
+    return _lib
+
+
+@pytest.fixture(scope="module")
+def subkeys(torch_dev, L):
+    torch, dev = torch_dev
+    from jeromq_amd import batch
+    k = torch.tensor(list(PRECOM), dtype=torch.uint8, device=dev).view(1, 32)
+    return torch.cat([batch.subkeys(k, L.CZ_DIR_C2S), batch.subkeys(k, L.CZ_DIR_S2C)])
+
+
+def _boundary_lengths(seg_blocks):
+    """Payload lengths whose box (n + 33 bytes) ends at every interesting offset
+    around segment boundaries, plus short frames that are never split."""
+    lens = [0, 1, 31, 64, 100, 4096]
+    for nblk in sorted({seg_blocks + seg_blocks // 2, seg_blocks + seg_blocks // 2 + 1, 2 * seg_blocks,
+                        2 * seg_blocks + 1, 3 * seg_blocks - 1, 5 * seg_blocks + 2, 1025}):
+        for r in (0, 1, 15, 16, 17, 31, 32, 33, 48, 63):
+            mlen = 64 * (nblk - 1) + (r if r else 64)
+            if mlen >= 33:
+                lens.append(mlen - 33)
+    lens.append(65536)
+    return lens
+
+
+def _pack(lens, shift=0, seed=0):
+    desc = np.zeros(len(lens), dtype=DESC_DTYPE)
+    io, oo = shift, 2 * shift + 1 if shift else 0
+    for i, n in enumerate(lens):
+        desc[i] = (io, oo, n, 0, 7 + 3 * i, i & 3, -1)   # or_seal_batch seals C2S
+        io += (n + 15) // 16 * 16
+        oo += (n + 33 + 15) // 16 * 16
+    hin = np.zeros(io + 64, dtype=np.uint8)
+    for i, n in enumerate(lens):
+        o = int(desc[i]["in_off"])
+        hin[o:o + n] = np.frombuffer(splitmix_bytes(n, seed + 77 * i), dtype=np.uint8)
+    return desc, hin, oo + 64
+
+
+def _oracle_seal(desc, hin, out_bytes):
+    out = np.zeros(out_bytes, dtype=np.uint8)
+    precom = np.frombuffer(PRECOM * 2, dtype=np.uint8)
+    oracle().or_seal_batch(desc.ctypes.data, len(desc), hin.ctypes.data, out.ctypes.data, precom.ctypes.data, 0, 8)
+    return out
+
+
+def _dev(torch_dev, a):
+    torch, dev = torch_dev
+    return torch.from_numpy(np.ascontiguousarray(a).view(np.uint8).copy()).to(dev)
+
+
+def _seal_seg(torch_dev, subkeys, desc, hin, ob, seg_blocks):
+    torch, dev = torch_dev
+    from jeromq_amd import batch
+    plan = batch.SegmentPlan(desc, open_=False, seg_blocks=seg_blocks).to(dev)
+    d_out = torch.zeros(ob, dtype=torch.uint8, device=dev)
+    batch.seal_segments(_dev(torch_dev, desc), plan, _dev(torch_dev, hin), d_out, subkeys, desc_np=desc)
+    torch.cuda.synchronize()
+    return d_out.cpu().numpy(), plan
+
+
+def _open_seg(torch_dev, subkeys, desc, hin, ob, seg_blocks):
+    torch, dev = torch_dev
+    from jeromq_amd import batch
+    plan = batch.SegmentPlan(desc, open_=True, seg_blocks=seg_blocks).to(dev)
+    d_out = torch.full((ob,), 0xA5, dtype=torch.uint8, device=dev)
+    status = torch.full((len(desc),), -1, dtype=torch.int16, device=dev)
+    nonces = torch.zeros(len(desc), dtype=torch.int64, device=dev)
+    batch.open_segments(_dev(torch_dev, desc), plan, _dev(torch_dev, hin), d_out, subkeys, status, nonces=nonces,
+                        desc_np=desc)
+    torch.cuda.synchronize()
+    return (status.cpu().numpy().view(np.uint16), d_out.cpu().numpy(), nonces.cpu().numpy().view(np.uint64), plan)
+
+
+@pytest.mark.parametrize("seg_blocks", [2, 3, 5, 64])
+@pytest.mark.parametrize("shift", [0, 3])
+def test_seal_segments_vs_oracle(torch_dev, subkeys, seg_blocks, shift):
+    lens = _boundary_lengths(seg_blocks)
+    desc, hin, ob = _pack(lens, shift=shift, seed=seg_blocks)
+    out, plan = _seal_seg(torch_dev, subkeys, desc, hin, ob, seg_blocks)
+    assert plan.ncomb > 0
+    want = _oracle_seal(desc, hin, ob)
+    assert np.array_equal(out, want)
+
+
+def _bodies(lens, seed):
+    bodies, meta = [], []
+    for i, n in enumerate(lens):
+        p = splitmix_bytes(n, seed + 31 * i)
+        ctr, fl, k = 11 + 2 * i, i & 3, i & 1
+        bodies.append(bytearray(or_curve_encode(p, fl, ctr, k, PRECOM)))
+        meta.append((p, fl, ctr, k))
+    return bodies, meta
+
+
+def _bodies_desc(bodies, meta, shift=0):
+    desc = np.zeros(len(bodies), dtype=DESC_DTYPE)
+    io, oo = shift, 3 if shift else 0
+    for i, b in enumerate(bodies):
+        desc[i] = (io, oo, len(b), meta[i][3], meta[i][2] - 1, 0x100, -1)
+        io += (len(b) + 15) // 16 * 16
+        oo += (max(len(b) - 33, 0) + 15) // 16 * 16
+    hin = np.zeros(io + 64, dtype=np.uint8)
+    for i, b in enumerate(bodies):
+        o = int(desc[i]["in_off"])
+        hin[o:o + len(b)] = np.frombuffer(bytes(b), dtype=np.uint8)
+    return desc, hin, oo + 64
+
+
+@pytest.mark.parametrize("seg_blocks", [2, 5, 64])
+@pytest.mark.parametrize("shift", [0, 5])
+def test_open_segments_roundtrip_and_tamper(torch_dev, subkeys, L, seg_blocks, shift):
+    lens = _boundary_lengths(seg_blocks)
+    bodies, meta = _bodies(lens, seed=1000 + seg_blocks)
+    want = [L.CZ_STATUS_OK] * len(bodies)
+    rng = np.random.default_rng(seg_blocks)
+    # tamper some split frames (tag, first/middle/last ciphertext byte) and reject others early
+    big = [i for i, b in enumerate(bodies) if len(b) > 64 * (seg_blocks + seg_blocks // 2)]
+    for j, i in enumerate(big[::3]):
+        b = bodies[i]
+        where = [16 + (j % 16), 33, 64 * seg_blocks + 7 if len(b) > 64 * seg_blocks + 7 else 40, len(b) - 1][j % 4]
+        b[where] ^= 1 << int(rng.integers(0, 8))
+        want[i] = L.CZ_STATUS_CRYPTO
+    for i in big[1::7]:
+        bodies[i][3] ^= 0x20          # header byte: COMMAND
+        want[i] = L.CZ_STATUS_COMMAND
+    desc, hin, ob = _bodies_desc(bodies, meta, shift=shift)
+    for i in big[2::11]:
+        if want[i] == L.CZ_STATUS_OK:
+            desc[i]["counter"] = meta[i][2]   # floor == nonce: replay
+            want[i] = L.CZ_STATUS_SEQUENCE
+    st, out, nn, plan = _open_seg(torch_dev, subkeys, desc, hin, ob, seg_blocks)
+    assert plan.ncomb > 0
+    assert list(st & 0xff) == want
+    for i, (p, fl, ctr, k) in enumerate(meta):
+        o = int(desc[i]["out_off"])
+        if want[i] == L.CZ_STATUS_OK:
+            assert st[i] >> 8 == fl, f"frame {i}"
+            assert out[o:o + len(p)].tobytes() == p, f"frame {i} len {len(p)}"
+        elif want[i] == L.CZ_STATUS_CRYPTO:
+            assert not out[o:o + len(p)].any(), f"frame {i} leaked plaintext"
+        if want[i] != L.CZ_STATUS_COMMAND:
+            assert nn[i] == ctr
+
+
+def test_segments_match_unsplit_kernels(torch_dev, subkeys):
+    """Zipf batch (the bench's ragged workload, up to 64 KiB): segmented == one lane per frame."""
+    torch, dev = torch_dev
+    from jeromq_amd import batch
+    rng = np.random.default_rng(7)
+    j = np.clip(rng.zipf(1.2, size=4000), 1, 1024)
+    lens = list((64 * j - rng.integers(0, 64, size=len(j))).astype(np.uint32))
+    desc, hin, ob = _pack([int(x) for x in lens], seed=5)
+    out_seg, _ = _seal_seg(torch_dev, subkeys, desc, hin, ob, 64)
+    d_out = torch.zeros(ob, dtype=torch.uint8, device=dev)
+    batch.seal_batch(_dev(torch_dev, desc), len(desc), _dev(torch_dev, hin), d_out, subkeys, desc_np=desc)
+    torch.cuda.synchronize()
+    assert np.array_equal(out_seg, d_out.cpu().numpy())

@@ -144,7 +144,8 @@ int cz_plan_order(const cz_frame_desc *h_desc, uint32_t count, uint32_t *h_order
  * One lane per frame makes a long frame the batch's critical path (a 64 KiB frame is
  * 1025 sequential Salsa20 blocks on one lane).  cz_plan_segments splits frames longer
  * than 1.5 x seg_blocks 64-byte blocks into seg_blocks-block segments (the last one
- * takes the remainder, 1..seg_blocks blocks), sorts segments longest first, and lists the split frames for
+ * takes the remainder; for open, segments s >= 1 start at block s*seg_blocks + 1),
+ * sorts segments longest first (by output chunks), and lists the split frames for
  * the combine step, which joins the per-segment Poly1305 partials with r^m powers.
  * d_work must hold 64 bytes per part (*npart from the planner).  Output contract as
  * cz_seal_batch / cz_open_batch (statuses, nonces, zeroed plaintext on a bad tag). */

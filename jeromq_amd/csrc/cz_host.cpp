@@ -347,14 +347,41 @@ int cz_plan_segments(const cz_frame_desc *h_desc, uint32_t count, int open, uint
             segs.push_back({i, 0u, nblk, 0xffffffffu});
             continue;
         }
-        const uint32_t ns = (nblk + seg_blocks - 1) / seg_blocks;  // last segment takes the remainder
+        // Seal segment s covers box blocks [s*seg, (s+1)*seg).  Open segments s >= 1 start one
+        // block later, at s*seg + 1, so each one's payload chunks start at s*seg: the 33-byte
+        // shift puts payload chunk g across box blocks g and g+1.  Last segment: the remainder.
+        const uint32_t lead = open ? 1u : 0u;
+        const uint32_t ns = (nblk - lead + seg_blocks - 1) / seg_blocks;
         combs.push_back({i, parts, ns, 0u});
-        for (uint32_t s = 0; s < ns; s++)
-            segs.push_back({i, s * seg_blocks, s + 1 < ns ? seg_blocks : nblk - s * seg_blocks, parts + s});
+        for (uint32_t s = 0; s < ns; s++) {
+            const uint32_t b0 = s ? s * seg_blocks + lead : 0u;
+            const uint32_t b1 = s + 1 < ns ? (s + 1) * seg_blocks + lead : nblk;
+            segs.push_back({i, b0, b1 - b0, parts + s});
+        }
         parts += ns;
     }
-    std::stable_sort(segs.begin(), segs.end(),
-                     [](const cz_segment &a, const cz_segment &b) { return a.nblocks > b.nblocks; });
+    // longest first, keyed on the kernel's loop count (output chunks), so that waves hold
+    // equal-length segments and can take the line-staged store path
+    auto chunks = [&](const cz_segment &g) -> uint32_t {
+        if (!open)
+            return g.nblocks;
+        const uint32_t len = h_desc[g.frame].len;
+        if (len < CZ_MESSAGE_OVERHEAD)
+            return 0u;
+        const uint32_t nblk = (len + 63) / 64, bend = g.first_block + g.nblocks;
+        const uint32_t cb = g.first_block ? g.first_block - 1 : 0u;
+        const uint32_t ce = bend == nblk ? (len - CZ_MESSAGE_OVERHEAD + 63) / 64 : bend - 1;
+        return ce - cb;
+    };
+    std::vector<std::pair<uint32_t, uint32_t>> key(segs.size());
+    for (size_t k = 0; k < segs.size(); k++)
+        key[k] = {chunks(segs[k]), (uint32_t)k};
+    std::stable_sort(key.begin(), key.end(), [](const std::pair<uint32_t, uint32_t> &a,
+                                                 const std::pair<uint32_t, uint32_t> &b) { return a.first > b.first; });
+    std::vector<cz_segment> sorted(segs.size());
+    for (size_t k = 0; k < segs.size(); k++)
+        sorted[k] = segs[key[k].second];
+    segs.swap(sorted);
     *nseg = (uint32_t)segs.size();
     *ncomb = (uint32_t)combs.size();
     *npart = parts;

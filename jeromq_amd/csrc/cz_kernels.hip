@@ -807,6 +807,10 @@ __device__ __forceinline__ u64 read_be64(const uint8_t *p)
 // Record: [0..4] h (2^32 radix, partially reduced), [5] poly blocks absorbed,
 // [6] decrypted flags byte (open, segment 0), [7] early status (open, segment 0),
 // [8..11] clamped r, [12..15] pad (segment 0).
+//
+// Both directions run ONE loop over the segment's output chunks with the emit
+// at the loop's convergence point, so a wave whose lanes hold segments with
+// the same chunk count can share the cooperative line emitter below.
 // ---------------------------------------------------------------------------
 template <bool AL>
 __device__ __forceinline__ u32 ld32(const uint8_t *__restrict__ p)
@@ -817,14 +821,99 @@ __device__ __forceinline__ u32 ld32(const uint8_t *__restrict__ p)
         return (u32)p[0] | ((u32)p[1] << 8) | ((u32)p[2] << 16) | ((u32)p[3] << 24);
 }
 
-template <bool AL>
-__device__ void seal_segment(const uint8_t *__restrict__ in, uint8_t *__restrict__ out, u32 n, u32 flags,
-                             u64 counter, const u32 key[8], u32 b0, u32 b1, u32 *__restrict__ rec)
+// Line staging for a wave of segments at arbitrary 16-byte aligned bases.  Like
+// EmitLines, 8 lanes write one 128-byte output line per store instruction, but
+// each lane's base and byte count come from a per-wave LDS table, and stores are
+// clipped to the segment's bytes (ragged frames are packed, nothing is padding).
+struct EmitSegLines {
+    uint4 *lds;      // this wave's 64 x 8 chunks
+    u64 *tbase;      // per-lane output base
+    u32 *ttot;       // per-lane byte count; bit 31: leave bytes 16..31 to tag()
+    uint8_t *mine;
+    u32 lane, total, last_q;
+
+    __device__ __forceinline__ void init(bool tag_slot)
+    {
+        tbase[lane] = (u64)(uintptr_t)mine;
+        ttot[lane] = total | (tag_slot ? 0x80000000u : 0u);
+    }
+    __device__ __forceinline__ void flush(u32 line)
+    {
+        const u32 c = lane & 7u;
+        const u32 r = lane >> 3;
+        const u32 off = 128u * line + 16u * c;
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+#pragma unroll
+        for (u32 j = 0; j < 8; j++) {
+            const u32 F = 8u * j + r;
+            const uint4 v = lds[F * 8u + (c ^ (F & 7u))];
+            const u32 tt = ttot[F];
+            const u32 tot = tt & 0x7fffffffu;
+            uint8_t *p = reinterpret_cast<uint8_t *>((uintptr_t)tbase[F]) + off;
+            const bool skip = (tt >> 31) && line == 0 && c == 1;
+            if (!skip) {
+                if (off + 16u <= tot)
+                    *reinterpret_cast<uint4 *>(p) = v;
+                else if (off < tot)
+                    st_bytes(p, v.x, v.y, v.z, v.w, tot - off);
+            }
+        }
+    }
+    __device__ __forceinline__ void emit(u32 q, const u32 D[16])
+    {
+        const u32 h = q & 1u;
+        const u32 sw = lane & 7u;
+#pragma unroll
+        for (u32 c = 0; c < 4; c++)
+            lds[lane * 8u + ((4u * h + c) ^ sw)] = make_uint4(D[4 * c], D[4 * c + 1], D[4 * c + 2], D[4 * c + 3]);
+        if (h)
+            flush(q >> 1);
+        last_q = q;
+    }
+    __device__ __forceinline__ void tag(const u32 t[4])
+    {
+        *reinterpret_cast<uint4 *>(mine + 16) = make_uint4(t[0], t[1], t[2], t[3]);
+    }
+    __device__ __forceinline__ void finish()
+    {
+        if ((last_q & 1u) == 0)
+            flush(last_q >> 1);  // bytes past the segment are clipped by the table's count
+    }
+    __device__ __forceinline__ void close(bool bad)
+    {
+        finish();
+        if (bad)
+            poison();
+    }
+    __device__ void poison()
+    {
+        __threadfence_block();  // land after the other lanes' stores of this lane's lines
+        for (u32 o = 0; o < total; o += 16) {
+            if (o + 16u <= total)
+                *reinterpret_cast<uint4 *>(mine + o) = make_uint4(0u, 0u, 0u, 0u);
+            else
+                st_bytes(mine + o, 0u, 0u, 0u, 0u, total - o);
+        }
+    }
+};
+
+// Bytes of box blocks [b0, bend) that go to the output of a seal segment.
+__device__ __forceinline__ u32 seal_seg_bytes(u32 mlen, u32 b0, u32 bend)
+{
+    const u32 e = 64u * bend < mlen ? 64u * bend : mlen;
+    return e - 64u * b0;
+}
+
+// Seal box blocks [b0, b1) of one MESSAGE.  Output chunk q is box block b0 + q
+// at em's base (body + 64*b0).  rec == nullptr: the whole frame, the tag goes
+// to bytes 16..31; otherwise the Poly1305 partial goes to rec.
+template <bool AL, class EM>
+__device__ void seal_segment(const uint8_t *__restrict__ in, u32 n, u32 flags, u64 counter, const u32 key[8], u32 b0,
+                             u32 b1, u32 *__restrict__ rec, EM &em)
 {
     const u32 mlen = n + 33u;
     const u32 nblk = (mlen + 63u) >> 6;
     const u32 nfull = mlen >> 6;
-    const u32 tailv = mlen & 63u;
     const u32 bend = b1 < nblk ? b1 : nblk;
     const u64 inlen = n;
     u32 n0, n1;
@@ -833,93 +922,71 @@ __device__ void seal_segment(const uint8_t *__restrict__ in, uint8_t *__restrict
     salsa20_block(x, key, n0, n1, 0u, 0u);
     Poly P;
     poly_init(P, x[0], x[1], x[2], x[3], x[4], x[5], x[6], x[7]);
-    EmitDirect<AL> em{out, mlen};
-    u32 carry, blk, mpoly = 0;
-    if (b0 == 0) {
-        V4 a = ld16<AL>(in, inlen);
-        V4 b = ld16<AL>(in + 16, inlen > 16 ? inlen - 16 : 0);
-        u32 W[9] = {flags << 24, a.x, a.y, a.z, a.w, b.x, b.y, b.z, b.w};
+    u32 carry = b0 == 0 ? (flags << 24) : ld32<AL>(in + 64u * b0 - 36u);  // payload dword P[16*b0 - 9]
+    u32 mpoly = 0;
+    for (u32 q = 0; q < bend - b0; q++) {
+        const u32 blk = b0 + q;
+        salsa20_block(x, key, n0, n1, blk, 0u);
+        if (blk == 0) {
+            V4 a = ld16<AL>(in, inlen);
+            V4 b = ld16<AL>(in + 16, inlen > 16 ? inlen - 16 : 0);
+            u32 W[9] = {carry, a.x, a.y, a.z, a.w, b.x, b.y, b.z, b.w};
 #pragma unroll
-        for (int k = 8; k < 16; k++)
-            C[k] = funnel(W[k - 7], W[k - 8], 3) ^ x[k];
-        carry = b.w;
-        C[0] = HDR0; C[1] = HDR1; C[2] = n0; C[3] = n1;
-        C[4] = C[5] = C[6] = C[7] = 0u;
-        if (nfull >= 1) {
+            for (int k = 8; k < 16; k++)
+                C[k] = funnel(W[k - 7], W[k - 8], 3) ^ x[k];
+            carry = b.w;
+            C[0] = HDR0; C[1] = HDR1; C[2] = n0; C[3] = n1;
+            C[4] = C[5] = C[6] = C[7] = 0u;
+        } else {
+            const uint8_t *src = in + 64u * blk - 32u;
+            V4 q0, q1, q2, q3;
+            if (blk < nfull) {
+                q0 = ld16f<AL>(src); q1 = ld16f<AL>(src + 16); q2 = ld16f<AL>(src + 32);
+                q3 = ld16<AL>(src + 48, inlen - (64u * blk + 16u));
+            } else {
+                const u64 o = 64u * blk - 32u;
+                q0 = ld16<AL>(src, o < inlen ? inlen - o : 0);
+                q1 = ld16<AL>(src + 16, o + 16 < inlen ? inlen - o - 16 : 0);
+                q2 = ld16<AL>(src + 32, o + 32 < inlen ? inlen - o - 32 : 0);
+                q3 = ld16<AL>(src + 48, o + 48 < inlen ? inlen - o - 48 : 0);
+            }
+            u32 W[17] = {carry, q0.x, q0.y, q0.z, q0.w, q1.x, q1.y, q1.z, q1.w,
+                         q2.x, q2.y, q2.z, q2.w, q3.x, q3.y, q3.z, q3.w};
+#pragma unroll
+            for (int k = 0; k < 16; k++)
+                C[k] = funnel(W[k + 1], W[k], 3) ^ x[k];
+            carry = q3.w;
+        }
+        if (blk != 0 && blk < nfull) {
+            poly_block(P, C[0], C[1], C[2], C[3], 1u);
+            poly_block(P, C[4], C[5], C[6], C[7], 1u);
             poly_block(P, C[8], C[9], C[10], C[11], 1u);
             poly_block(P, C[12], C[13], C[14], C[15], 1u);
-            mpoly = 2;
+            mpoly += 4;
         } else {
-            u32 nb = mlen - 32u;
-            if (nb >= 16u) {
-                poly_block(P, C[8], C[9], C[10], C[11], 1u);
-                if (nb > 16u)
-                    poly_block_partial(P, C[12], C[13], C[14], C[15], nb - 16u);
-            } else {
-                poly_block_partial(P, C[8], C[9], C[10], C[11], nb);
-            }
-            mpoly = (nb + 15u) >> 4;
-        }
-        em.emit(0, C);
-        blk = 1;
-    } else {
-        carry = ld32<AL>(in + 64u * b0 - 36u);  // payload dword P[16*b0 - 9]
-        blk = b0;
-    }
-    const u32 fend = nfull < bend ? nfull : bend;
-    for (; blk < fend; blk++) {
-        const uint8_t *src = in + 64u * blk - 32u;
-        V4 q0 = ld16f<AL>(src), q1 = ld16f<AL>(src + 16), q2 = ld16f<AL>(src + 32);
-        V4 q3 = ld16<AL>(src + 48, inlen - (64u * blk + 16u));
-        u32 W[17] = {carry, q0.x, q0.y, q0.z, q0.w, q1.x, q1.y, q1.z, q1.w,
-                     q2.x, q2.y, q2.z, q2.w, q3.x, q3.y, q3.z, q3.w};
-        salsa20_block(x, key, n0, n1, blk, 0u);
 #pragma unroll
-        for (int k = 0; k < 16; k++)
-            C[k] = funnel(W[k + 1], W[k], 3) ^ x[k];
-        carry = q3.w;
-        poly_block(P, C[0], C[1], C[2], C[3], 1u);
-        poly_block(P, C[4], C[5], C[6], C[7], 1u);
-        poly_block(P, C[8], C[9], C[10], C[11], 1u);
-        poly_block(P, C[12], C[13], C[14], C[15], 1u);
-        mpoly += 4;
-        em.emit(blk, C);
-    }
-    if (tailv != 0 && nfull >= 1 && nfull < bend) {
-        const u32 tb = nfull;
-        V4 q[4];
-#pragma unroll
-        for (int c = 0; c < 4; c++) {
-            long o = (long)(64u * tb) - 32 + 16 * c;
-            u64 avail = (o >= 0 && (u64)o < inlen) ? inlen - (u64)o : 0;
-            q[c] = ld16<AL>(in + o, avail);
-        }
-        salsa20_block(x, key, n0, n1, tb, 0u);
-        u32 W[17] = {carry, q[0].x, q[0].y, q[0].z, q[0].w, q[1].x, q[1].y, q[1].z, q[1].w,
-                     q[2].x, q[2].y, q[2].z, q[2].w, q[3].x, q[3].y, q[3].z, q[3].w};
-#pragma unroll
-        for (int k = 0; k < 16; k++)
-            C[k] = funnel(W[k + 1], W[k], 3) ^ x[k];
-#pragma unroll
-        for (int j = 0; j < 4; j++) {
-            u32 s = 16u * j;
-            if (s < tailv) {
-                u32 nb = tailv - s;
-                if (nb >= 16)
-                    poly_block(P, C[4 * j], C[4 * j + 1], C[4 * j + 2], C[4 * j + 3], 1u);
-                else
-                    poly_block_partial(P, C[4 * j], C[4 * j + 1], C[4 * j + 2], C[4 * j + 3], nb);
+            for (int j = 0; j < 4; j++) {
+                const u32 s = 64u * blk + 16u * j;
+                if (s >= 32u && s < mlen) {
+                    const u32 nb = mlen - s;
+                    if (nb >= 16)
+                        poly_block(P, C[4 * j], C[4 * j + 1], C[4 * j + 2], C[4 * j + 3], 1u);
+                    else
+                        poly_block_partial(P, C[4 * j], C[4 * j + 1], C[4 * j + 2], C[4 * j + 3], nb);
+                    mpoly++;
+                }
             }
         }
-        mpoly += (tailv + 15u) >> 4;
-        em.emit(tb, C);
+        em.emit(q, C);
     }
     if (!rec) {
         u32 tag[4];
         poly_finish(P, tag);
         em.tag(tag);
+        em.close(false);
         return;
     }
+    em.close(false);
     rec[0] = P.h0; rec[1] = P.h1; rec[2] = P.h2; rec[3] = P.h3; rec[4] = P.h4; rec[5] = mpoly;
     if (b0 == 0) {
         rec[8] = P.r0; rec[9] = P.r1; rec[10] = P.r2; rec[11] = P.r3;
@@ -927,143 +994,158 @@ __device__ void seal_segment(const uint8_t *__restrict__ in, uint8_t *__restrict
     }
 }
 
-// Open one segment [b0, b1) of a MESSAGE body.  Emits payload chunks
-// [b0-1, b1-1) (the 33-byte shift lags the payload one block behind the body),
-// so a segment with b0 > 0 first recomputes block b0-1's plaintext tail.
-template <bool AL>
-__device__ u32 open_segment(const uint8_t *__restrict__ in, uint8_t *__restrict__ out, u32 size, const u32 key[8],
-                            bool check_floor, long long floor, u32 *flags_out, u64 *nonce_out, u32 b0, u32 b1,
-                            u32 *__restrict__ rec)
+// MESSAGE header checks of ZmqCurveMechanism.decode (order: command, malformed,
+// sequence); on OK returns the nonce words.  See open_frame for the citations.
+__device__ __forceinline__ u32 open_header(const uint8_t *__restrict__ in, u32 size, bool check_floor,
+                                           long long floor, u32 &n0, u32 &n1, u64 &nonce)
 {
-    V4 h = ld16<AL>(in, size);
-    if (size < 8u || h.x != HDR0 || (h.y & 0x00ffffffu) != (HDR1 & 0x00ffffffu))
+    if (size < 8u)
+        return CZ_STATUS_COMMAND;
+    V4 h = ld16<false>(in, size);
+    if (h.x != HDR0 || (h.y & 0x00ffffffu) != (HDR1 & 0x00ffffffu))
         return CZ_STATUS_COMMAND;
     if (size < 33u)
         return CZ_STATUS_MALFORMED;
-    const u32 n0 = h.z, n1 = h.w;
-    const u64 nonce = ((u64)bswap32(n0) << 32) | (u64)bswap32(n1);
-    *nonce_out = nonce;
+    n0 = h.z;
+    n1 = h.w;
+    nonce = ((u64)bswap32(n0) << 32) | (u64)bswap32(n1);
     if (check_floor && (long long)nonce <= floor)
         return CZ_STATUS_SEQUENCE;
+    return CZ_STATUS_OK;
+}
 
+// Open segment geometry.  Segment 0 MACs box blocks [0, b1); segment s >= 1
+// starts at block b0 = s*SEG + 1 and MACs [b0, b1).  Payload chunk g (bytes
+// 64g..64g+63) needs box blocks g and g+1, so the segment emits chunks
+// [cb, ce) with cb = b0 ? b0 - 1 : 0 and ce = b1 - 1, or every remaining chunk
+// when b1 reaches the end of the box.
+struct OpenSeg {
+    u32 nblk, nout, cb, ce, bend;
+};
+__device__ __forceinline__ OpenSeg open_seg_geom(u32 size, u32 b0, u32 b1)
+{
+    OpenSeg g;
+    g.nblk = (size + 63u) >> 6;
+    g.nout = size - 33u;
+    g.bend = b1 < g.nblk ? b1 : g.nblk;
+    g.cb = b0 ? b0 - 1u : 0u;
+    g.ce = g.bend == g.nblk ? (g.nout + 63u) >> 6 : g.bend - 1u;
+    return g;
+}
+
+// Open box blocks [b0, b1) of one MESSAGE body whose header passed open_header.
+// Returns CZ_STATUS_OK or (whole frame, bad tag) CZ_STATUS_CRYPTO.
+template <bool AL, class EM>
+__device__ u32 open_segment(const uint8_t *__restrict__ in, u32 size, const u32 key[8], u32 n0, u32 n1, u32 b0,
+                            u32 b1, u32 *__restrict__ rec, u32 &flags_out, EM &em)
+{
+    const OpenSeg g = open_seg_geom(size, b0, b1);
     const u32 mlen = size;
-    const u32 nblk = (mlen + 63u) >> 6;
     const u32 nfull = mlen >> 6;
-    const u32 nout = size - 33u;
-    const u32 bend = b1 < nblk ? b1 : nblk;
-    u32 x[16], C[16], X[16], K[8];
+    u32 x[16], X[16], K[8];
     salsa20_block(x, key, n0, n1, 0u, 0u);
     Poly P;
     poly_init(P, x[0], x[1], x[2], x[3], x[4], x[5], x[6], x[7]);
-    EmitDirect<AL> em{out, nout};
-    u32 blk, mpoly = 0;
+    u32 mpoly = 0;
+    // prologue: plaintext dwords 8..15 of block cb (MACed here only for segment 0)
     if (b0 == 0) {
         V4 a = ld16<AL>(in + 32, size > 32 ? size - 32u : 0);
         V4 b = ld16<AL>(in + 48, size > 48 ? size - 48u : 0);
-        C[8] = a.x; C[9] = a.y; C[10] = a.z; C[11] = a.w;
-        C[12] = b.x; C[13] = b.y; C[14] = b.z; C[15] = b.w;
-        if (nfull >= 1) {
-            poly_block(P, C[8], C[9], C[10], C[11], 1u);
-            poly_block(P, C[12], C[13], C[14], C[15], 1u);
-            mpoly = 2;
-        } else {
-            u32 nb = mlen - 32u;
-            if (nb >= 16u) {
-                poly_block(P, C[8], C[9], C[10], C[11], 1u);
-                if (nb > 16u)
-                    poly_block_partial(P, C[12], C[13], C[14], C[15], nb - 16u);
-            } else {
-                poly_block_partial(P, C[8], C[9], C[10], C[11], nb);
+        const u32 nb = (mlen < 64u ? mlen : 64u) - 32u;
+        if (nb >= 16u) {
+            poly_block(P, a.x, a.y, a.z, a.w, 1u);
+            mpoly++;
+            if (nb >= 32u) {
+                poly_block(P, b.x, b.y, b.z, b.w, 1u);
+                mpoly++;
+            } else if (nb > 16u) {
+                poly_block_partial(P, b.x, b.y, b.z, b.w, nb - 16u);
+                mpoly++;
             }
-            mpoly = (nb + 15u) >> 4;
+        } else if (nb > 0u) {
+            poly_block_partial(P, a.x, a.y, a.z, a.w, nb);
+            mpoly++;
         }
-#pragma unroll
-        for (int k = 0; k < 8; k++)
-            K[k] = C[8 + k] ^ x[8 + k];
-        *flags_out = K[0] & 0xffu;
-        blk = 1;
+        K[0] = a.x ^ x[8]; K[1] = a.y ^ x[9]; K[2] = a.z ^ x[10]; K[3] = a.w ^ x[11];
+        K[4] = b.x ^ x[12]; K[5] = b.y ^ x[13]; K[6] = b.z ^ x[14]; K[7] = b.w ^ x[15];
+        flags_out = K[0] & 0xffu;
     } else {
-        // plaintext dwords 8..15 of block b0-1 (its MAC belongs to the previous segment)
-        salsa20_block(X, key, n0, n1, b0 - 1u, 0u);
-        const uint8_t *src = in + 64u * (b0 - 1u) + 32u;
+        salsa20_block(X, key, n0, n1, g.cb, 0u);
+        const uint8_t *src = in + 64u * g.cb + 32u;
         V4 a = ld16f<AL>(src), b = ld16f<AL>(src + 16);
         K[0] = a.x ^ X[8]; K[1] = a.y ^ X[9]; K[2] = a.z ^ X[10]; K[3] = a.w ^ X[11];
         K[4] = b.x ^ X[12]; K[5] = b.y ^ X[13]; K[6] = b.z ^ X[14]; K[7] = b.w ^ X[15];
-        blk = b0;
     }
-    for (; blk < bend; blk++) {
-        const uint8_t *src = in + 64u * blk;
-        const bool full = blk < nfull;
-        V4 q0, q1, q2, q3;
-        if (full) {
-            q0 = ld16f<AL>(src); q1 = ld16f<AL>(src + 16); q2 = ld16f<AL>(src + 32); q3 = ld16f<AL>(src + 48);
-        } else {
-            const u32 o = 64u * blk;
-            q0 = ld16<AL>(src, size - o);
-            q1 = ld16<AL>(src + 16, o + 16u < size ? size - o - 16u : 0);
-            q2 = ld16<AL>(src + 32, o + 32u < size ? size - o - 32u : 0);
-            q3 = ld16<AL>(src + 48, o + 48u < size ? size - o - 48u : 0);
-        }
-        C[0] = q0.x; C[1] = q0.y; C[2] = q0.z; C[3] = q0.w;
-        C[4] = q1.x; C[5] = q1.y; C[6] = q1.z; C[7] = q1.w;
-        C[8] = q2.x; C[9] = q2.y; C[10] = q2.z; C[11] = q2.w;
-        C[12] = q3.x; C[13] = q3.y; C[14] = q3.z; C[15] = q3.w;
-        salsa20_block(x, key, n0, n1, blk, 0u);
-        if (full) {
-            poly_block(P, C[0], C[1], C[2], C[3], 1u);
-            poly_block(P, C[4], C[5], C[6], C[7], 1u);
-            poly_block(P, C[8], C[9], C[10], C[11], 1u);
-            poly_block(P, C[12], C[13], C[14], C[15], 1u);
-            mpoly += 4;
-        } else {
-            const u32 tailv = mlen - 64u * blk;
+    for (u32 q = 0; q < g.ce - g.cb; q++) {
+        const u32 blk = g.cb + q + 1u;  // chunk cb+q needs box block cb+q+1
+        if (blk < g.nblk) {
+            const uint8_t *src = in + 64u * blk;
+            V4 q0, q1, q2, q3;
+            const bool full = blk < nfull;
+            if (full) {
+                q0 = ld16f<AL>(src); q1 = ld16f<AL>(src + 16); q2 = ld16f<AL>(src + 32); q3 = ld16f<AL>(src + 48);
+            } else {
+                const u32 o = 64u * blk;
+                q0 = ld16<AL>(src, size - o);
+                q1 = ld16<AL>(src + 16, o + 16u < size ? size - o - 16u : 0);
+                q2 = ld16<AL>(src + 32, o + 32u < size ? size - o - 32u : 0);
+                q3 = ld16<AL>(src + 48, o + 48u < size ? size - o - 48u : 0);
+            }
+            u32 C[16] = {q0.x, q0.y, q0.z, q0.w, q1.x, q1.y, q1.z, q1.w,
+                         q2.x, q2.y, q2.z, q2.w, q3.x, q3.y, q3.z, q3.w};
+            salsa20_block(x, key, n0, n1, blk, 0u);
+            if (full) {
+                poly_block(P, C[0], C[1], C[2], C[3], 1u);
+                poly_block(P, C[4], C[5], C[6], C[7], 1u);
+                poly_block(P, C[8], C[9], C[10], C[11], 1u);
+                poly_block(P, C[12], C[13], C[14], C[15], 1u);
+                mpoly += 4;
+            } else {
+                const u32 tailv = mlen - 64u * blk;
 #pragma unroll
-            for (int j = 0; j < 4; j++) {
-                u32 s = 16u * j;
-                if (s < tailv) {
-                    u32 nb = tailv - s;
-                    if (nb >= 16)
-                        poly_block(P, C[4 * j], C[4 * j + 1], C[4 * j + 2], C[4 * j + 3], 1u);
-                    else
-                        poly_block_partial(P, C[4 * j], C[4 * j + 1], C[4 * j + 2], C[4 * j + 3], nb);
+                for (int j = 0; j < 4; j++) {
+                    const u32 s = 16u * j;
+                    if (s < tailv) {
+                        const u32 nb = tailv - s;
+                        if (nb >= 16)
+                            poly_block(P, C[4 * j], C[4 * j + 1], C[4 * j + 2], C[4 * j + 3], 1u);
+                        else
+                            poly_block_partial(P, C[4 * j], C[4 * j + 1], C[4 * j + 2], C[4 * j + 3], nb);
+                        mpoly++;
+                    }
                 }
             }
-            mpoly += (tailv + 15u) >> 4;
-        }
 #pragma unroll
-        for (int k = 0; k < 16; k++)
-            X[k] = C[k] ^ x[k];
+            for (int k = 0; k < 16; k++)
+                X[k] = C[k] ^ x[k];
+        } else {
+#pragma unroll
+            for (int k = 0; k < 16; k++)
+                X[k] = 0u;
+        }
         u32 O[16];
         u32 E[17] = {K[0], K[1], K[2], K[3], K[4], K[5], K[6], K[7], X[0], X[1], X[2], X[3], X[4], X[5], X[6], X[7],
                      X[8]};
 #pragma unroll
         for (int t = 0; t < 16; t++)
             O[t] = funnel(E[t + 1], E[t], 1);
-        em.emit(blk - 1u, O);
+        em.emit(q, O);
 #pragma unroll
         for (int k = 0; k < 8; k++)
             K[k] = X[8 + k];
-    }
-    if (bend == nblk && 64u * (nblk - 1u) < nout) {
-        u32 O[16];
-#pragma unroll
-        for (int t = 0; t < 16; t++)
-            O[t] = t < 7 ? funnel(K[t + 1], K[t], 1) : (t == 7 ? funnel(0u, K[7], 1) : 0u);
-        em.emit(nblk - 1u, O);
     }
     if (!rec) {
         u32 tag[4];
         poly_finish(P, tag);
         V4 tin = ld16<AL>(in + 16, size - 16u);
-        if ((tag[0] ^ tin.x) | (tag[1] ^ tin.y) | (tag[2] ^ tin.z) | (tag[3] ^ tin.w)) {
-            em.poison();
-            return CZ_STATUS_CRYPTO;
-        }
-        return CZ_STATUS_OK;
+        const bool bad = ((tag[0] ^ tin.x) | (tag[1] ^ tin.y) | (tag[2] ^ tin.z) | (tag[3] ^ tin.w)) != 0;
+        em.close(bad);
+        return bad ? CZ_STATUS_CRYPTO : CZ_STATUS_OK;
     }
+    em.close(false);
     rec[0] = P.h0; rec[1] = P.h1; rec[2] = P.h2; rec[3] = P.h3; rec[4] = P.h4; rec[5] = mpoly;
     if (b0 == 0) {
-        rec[6] = *flags_out;
+        rec[6] = flags_out;
         rec[8] = P.r0; rec[9] = P.r1; rec[10] = P.r2; rec[11] = P.r3;
         rec[12] = P.p0; rec[13] = P.p1; rec[14] = P.p2; rec[15] = P.p3;
     }
@@ -1281,27 +1363,60 @@ __global__ __launch_bounds__(BLOCK) void k_open_uniform(const uint8_t *__restric
 
 
 // ---- segmented (ragged) batches ------------------------------------------
+constexpr u32 SEG_LDS_BYTES = LINE_LDS_BYTES + 64 * 8 + 64 * 4;  // chunks + base/count table per wave
+
+// A wave takes the line emitter when all 64 lanes hold segments with the same
+// chunk count and 16-byte aligned input/output; otherwise each lane stores directly.
+__device__ __forceinline__ bool wave_lines_ok(bool full_wave, u32 nchunks, bool al)
+{
+    if (!full_wave)
+        return false;
+    return wave_uniform(nchunks) && __builtin_amdgcn_ballot_w64(!al) == 0;
+}
+
 __global__ __launch_bounds__(BLOCK) void k_seal_segments(const cz_frame_desc *__restrict__ desc,
                                                           const cz_segment *__restrict__ segs, uint32_t nseg,
                                                           const uint8_t *__restrict__ in, uint8_t *__restrict__ out,
                                                           const uint8_t *__restrict__ subkeys,
-                                                          u32 *__restrict__ work)
+                                                          u32 *__restrict__ work, int allow_lines)
 {
+    extern __shared__ uint4 smem[];
     const uint32_t t = blockIdx.x * BLOCK + threadIdx.x;
-    if (t >= nseg)
+    const uint32_t wave_first = t & ~63u;
+    if (wave_first >= nseg)
         return;
-    const cz_segment sg = segs[t];
+    const bool live = t < nseg;
+    const cz_segment sg = segs[live ? t : wave_first];
     const cz_frame_desc d = desc[sg.frame];
     u32 key[8];
     load_key(subkeys + 32ull * d.key_idx, key);
     u32 *rec = sg.part == 0xffffffffu ? nullptr : work + 16ull * sg.part;
     const uint8_t *src = in + d.in_off;
-    uint8_t *dst = out + d.out_off;
+    uint8_t *dst = out + d.out_off + 64ull * sg.first_block;
     const u32 b1 = sg.first_block + sg.nblocks;
-    if (aligned16(src, dst))
-        seal_segment<true>(src, dst, d.len, d.flags & 0xffu, d.counter, key, sg.first_block, b1, rec);
-    else
-        seal_segment<false>(src, dst, d.len, d.flags & 0xffu, d.counter, key, sg.first_block, b1, rec);
+    const u32 mlen = d.len + 33u;
+    const u32 nblk = (mlen + 63u) >> 6;
+    const u32 nch = (b1 < nblk ? b1 : nblk) - sg.first_block;
+    const u32 total = seal_seg_bytes(mlen, sg.first_block, b1 < nblk ? b1 : nblk);
+    const bool al = aligned16(src, dst);
+    if (allow_lines && wave_lines_ok(wave_first + 64u <= nseg, nch, al)) {
+        const u32 lane = threadIdx.x & 63u;
+        uint8_t *wl = reinterpret_cast<uint8_t *>(smem) + (threadIdx.x >> 6) * SEG_LDS_BYTES;
+        EmitSegLines em{reinterpret_cast<uint4 *>(wl), reinterpret_cast<u64 *>(wl + LINE_LDS_BYTES),
+                        reinterpret_cast<u32 *>(wl + LINE_LDS_BYTES + 512), dst, lane, total, 0u};
+        em.init(sg.first_block == 0);
+        seal_segment<true>(src, d.len, d.flags & 0xffu, d.counter, key, sg.first_block, b1, rec, em);
+        return;
+    }
+    if (!live)
+        return;
+    if (al) {
+        EmitDirect<true> em{dst, total};
+        seal_segment<true>(src, d.len, d.flags & 0xffu, d.counter, key, sg.first_block, b1, rec, em);
+    } else {
+        EmitDirect<false> em{dst, total};
+        seal_segment<false>(src, d.len, d.flags & 0xffu, d.counter, key, sg.first_block, b1, rec, em);
+    }
 }
 
 __global__ __launch_bounds__(BLOCK) void k_seal_combine(const cz_frame_desc *__restrict__ desc,
@@ -1327,41 +1442,71 @@ __global__ __launch_bounds__(BLOCK) void k_open_segments(const cz_frame_desc *__
                                                           const uint8_t *__restrict__ in, uint8_t *__restrict__ out,
                                                           const uint8_t *__restrict__ subkeys,
                                                           u32 *__restrict__ work, uint16_t *__restrict__ status,
-                                                          uint64_t *__restrict__ nonces)
+                                                          uint64_t *__restrict__ nonces, int allow_lines)
 {
+    extern __shared__ uint4 smem[];
     const uint32_t t = blockIdx.x * BLOCK + threadIdx.x;
-    if (t >= nseg)
+    const uint32_t wave_first = t & ~63u;
+    if (wave_first >= nseg)
         return;
-    const cz_segment sg = segs[t];
+    const bool live = t < nseg;
+    const cz_segment sg = segs[live ? t : wave_first];
     const cz_frame_desc d = desc[sg.frame];
-    u32 key[8];
-    load_key(subkeys + 32ull * d.key_idx, key);
     long long floor = (long long)d.counter;
     if (d.prev >= 0)
         floor = (long long)read_be64(in + desc[d.prev].in_off + 8);
     const bool check = (d.flags & CZ_DESC_CHECK_NONCE) != 0;
     const uint8_t *src = in + d.in_off;
-    uint8_t *dst = out + d.out_off;
-    u32 *rec = sg.part == 0xffffffffu ? nullptr : work + 16ull * sg.part;
-    u32 fl = 0;
+    u32 n0 = 0, n1 = 0;
     u64 nonce = 0;
-    const u32 b1 = sg.first_block + sg.nblocks;
-    u32 st;
-    if (aligned16(src, dst))
-        st = open_segment<true>(src, dst, d.len, key, check, floor, &fl, &nonce, sg.first_block, b1, rec);
-    else
-        st = open_segment<false>(src, dst, d.len, key, check, floor, &fl, &nonce, sg.first_block, b1, rec);
-    if (sg.first_block == 0) {
+    const u32 early = open_header(src, d.len, check, floor, n0, n1, nonce);
+    u32 *rec = sg.part == 0xffffffffu ? nullptr : work + 16ull * sg.part;
+    const bool seg0 = sg.first_block == 0;
+    if (live && seg0) {
         if (nonces)
             nonces[sg.frame] = nonce;
+        if (rec)
+            rec[7] = early;  // the combine kernel finishes frames whose header passed
+        if (early != CZ_STATUS_OK)
+            status[sg.frame] = (uint16_t)early;
+    }
+    u32 key[8];
+    load_key(subkeys + 32ull * d.key_idx, key);
+    const u32 b1 = sg.first_block + sg.nblocks;
+    OpenSeg g{};
+    u32 nch = 0;
+    if (early == CZ_STATUS_OK) {
+        g = open_seg_geom(d.len, sg.first_block, b1);
+        nch = g.ce - g.cb;
+    }
+    uint8_t *dst = out + d.out_off + 64ull * g.cb;
+    const u32 total = early == CZ_STATUS_OK ? (g.bend == g.nblk ? g.nout : 64u * g.ce) - 64u * g.cb : 0u;
+    const bool al = aligned16(src, dst);
+    u32 fl = 0;
+    if (allow_lines && wave_lines_ok(wave_first + 64u <= nseg, nch, al) &&
+        __builtin_amdgcn_ballot_w64(early != CZ_STATUS_OK) == 0) {
+        const u32 lane = threadIdx.x & 63u;
+        uint8_t *wl = reinterpret_cast<uint8_t *>(smem) + (threadIdx.x >> 6) * SEG_LDS_BYTES;
+        EmitSegLines em{reinterpret_cast<uint4 *>(wl), reinterpret_cast<u64 *>(wl + LINE_LDS_BYTES),
+                        reinterpret_cast<u32 *>(wl + LINE_LDS_BYTES + 512), dst, lane, total, 0u};
+        em.init(false);
+        const u32 st = open_segment<true>(src, d.len, key, n0, n1, sg.first_block, b1, rec, fl, em);
         if (!rec)
             status[sg.frame] = (uint16_t)(st | (st == CZ_STATUS_OK ? (fl << 8) : 0u));
-        else {
-            rec[7] = st;  // early rejects are final; the combine kernel finishes OK frames
-            if (st != CZ_STATUS_OK)
-                status[sg.frame] = (uint16_t)st;
-        }
+        return;
     }
+    if (!live || early != CZ_STATUS_OK)
+        return;
+    u32 st;
+    if (al) {
+        EmitDirect<true> em{dst, total};
+        st = open_segment<true>(src, d.len, key, n0, n1, sg.first_block, b1, rec, fl, em);
+    } else {
+        EmitDirect<false> em{dst, total};
+        st = open_segment<false>(src, d.len, key, n0, n1, sg.first_block, b1, rec, fl, em);
+    }
+    if (!rec)
+        status[sg.frame] = (uint16_t)(st | (st == CZ_STATUS_OK ? (fl << 8) : 0u));
 }
 
 __global__ __launch_bounds__(BLOCK) void k_open_combine(const cz_frame_desc *__restrict__ desc,
@@ -1495,6 +1640,7 @@ int pick_staging(uint64_t stride, uint32_t out_bytes, bool aligned)
 // run-time tuning knobs (cz_tune): whole-line input loads for the uniform kernels
 static int g_pair = 1;
 static int g_un0 = 1;  // scalar first Salsa round when the high nonce word is wave-uniform
+static int g_seglines = 1;  // line-staged stores for waves of equal-length segments
 
 // ---------------------------------------------------------------------------
 // Launchers (called from cz_host.cpp).  No allocation, no synchronisation:
@@ -1603,8 +1749,9 @@ hipError_t czk_seal_segments(const cz_frame_desc *desc, const cz_segment *segs, 
                              uint32_t ncomb, const void *in, void *out, const void *subkeys, void *work, hipStream_t s)
 {
     if (nseg)
-        hipLaunchKernelGGL(k_seal_segments, dim3((nseg + BLOCK - 1) / BLOCK), dim3(BLOCK), 0, s, desc, segs, nseg,
-                           (const uint8_t *)in, (uint8_t *)out, (const uint8_t *)subkeys, (u32 *)work);
+        hipLaunchKernelGGL(k_seal_segments, dim3((nseg + BLOCK - 1) / BLOCK), dim3(BLOCK), WAVES * SEG_LDS_BYTES, s,
+                           desc, segs, nseg, (const uint8_t *)in, (uint8_t *)out, (const uint8_t *)subkeys,
+                           (u32 *)work, g_seglines);
     if (ncomb)
         hipLaunchKernelGGL(k_seal_combine, dim3((ncomb + BLOCK - 1) / BLOCK), dim3(BLOCK), 0, s, desc, comb, ncomb,
                            (uint8_t *)out, (const u32 *)work);
@@ -1616,8 +1763,9 @@ hipError_t czk_open_segments(const cz_frame_desc *desc, const cz_segment *segs, 
                              uint16_t *status, uint64_t *nonces, hipStream_t s)
 {
     if (nseg)
-        hipLaunchKernelGGL(k_open_segments, dim3((nseg + BLOCK - 1) / BLOCK), dim3(BLOCK), 0, s, desc, segs, nseg,
-                           (const uint8_t *)in, (uint8_t *)out, (const uint8_t *)subkeys, (u32 *)work, status, nonces);
+        hipLaunchKernelGGL(k_open_segments, dim3((nseg + BLOCK - 1) / BLOCK), dim3(BLOCK), WAVES * SEG_LDS_BYTES, s,
+                           desc, segs, nseg, (const uint8_t *)in, (uint8_t *)out, (const uint8_t *)subkeys,
+                           (u32 *)work, status, nonces, g_seglines);
     if (ncomb)
         hipLaunchKernelGGL(k_open_combine, dim3((ncomb + BLOCK - 1) / BLOCK), dim3(BLOCK), 0, s, desc, comb, ncomb,
                            (const uint8_t *)in, (uint8_t *)out, (const u32 *)work, status);
@@ -1636,6 +1784,11 @@ int czk_tune(const char *key, int value)
     if (key[0] == 'u' && key[1] == 'n' && key[2] == '0' && key[3] == 0) {
         int old = g_un0;
         g_un0 = value != 0;
+        return old;
+    }
+    if (__builtin_strcmp(key, "seglines") == 0) {
+        int old = g_seglines;
+        g_seglines = value != 0;
         return old;
     }
     return -1;

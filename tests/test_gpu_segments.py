@@ -187,3 +187,47 @@ def test_segments_match_unsplit_kernels(torch_dev, subkeys):
     batch.seal_batch(_dev(torch_dev, desc), len(desc), _dev(torch_dev, hin), d_out, subkeys, desc_np=desc)
     torch.cuda.synchronize()
     assert np.array_equal(out_seg, d_out.cpu().numpy())
+
+
+@pytest.mark.parametrize("seglines", [1, 0])
+def test_zipf_seal_open_line_and_direct_stores(torch_dev, subkeys, L, seglines):
+    """Both store paths of the segment kernels (cz_tune "seglines"): a Zipf batch
+    sealed vs the oracle, then opened with tampered and replayed frames mixed in."""
+    lib = L.lib()
+    old = lib.cz_tune(b"seglines", seglines)
+    try:
+        rng = np.random.default_rng(11 + seglines)
+        j = np.clip(rng.zipf(1.2, size=3000), 1, 1024)
+        lens = [int(x) for x in (64 * j - rng.integers(0, 64, size=len(j)))]
+        desc, hin, ob = _pack(lens, seed=17)
+        out, _ = _seal_seg(torch_dev, subkeys, desc, hin, ob, 64)
+        assert np.array_equal(out, _oracle_seal(desc, hin, ob))
+        # open the sealed bodies in place of the oracle's (identical, checked above)
+        bodies, meta = [], []
+        for i, n in enumerate(lens):
+            o = int(desc[i]["out_off"])
+            bodies.append(bytearray(out[o:o + n + 33].tobytes()))
+            o_in = int(desc[i]["in_off"])
+            meta.append((hin[o_in:o_in + n].tobytes(), int(desc[i]["flags"]), int(desc[i]["counter"]), 0))
+        want = [L.CZ_STATUS_OK] * len(bodies)
+        for i in rng.choice(len(bodies), size=40, replace=False):
+            b = bodies[i]
+            b[int(rng.integers(16, len(b)))] ^= 0x10
+            want[i] = L.CZ_STATUS_CRYPTO
+        odesc, ohin, oob = _bodies_desc(bodies, meta)
+        for i in rng.choice(len(bodies), size=10, replace=False):
+            if want[i] == L.CZ_STATUS_OK:
+                odesc[i]["counter"] = meta[i][2] + 1
+                want[i] = L.CZ_STATUS_SEQUENCE
+        st, pout, nn, plan = _open_seg(torch_dev, subkeys, odesc, ohin, oob, 64)
+        assert list(st & 0xff) == want
+        for i, (p, fl, ctr, k) in enumerate(meta):
+            o = int(odesc[i]["out_off"])
+            if want[i] == L.CZ_STATUS_OK:
+                assert st[i] >> 8 == fl
+                assert pout[o:o + len(p)].tobytes() == p, f"frame {i} len {len(p)}"
+            elif want[i] == L.CZ_STATUS_CRYPTO:
+                assert not pout[o:o + len(p)].any()
+            assert nn[i] == ctr
+    finally:
+        lib.cz_tune(b"seglines", old)

@@ -38,6 +38,9 @@ def parse():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--seg-blocks", type=int, default=64, help="zipf: segment length in 64-byte blocks")
+    ap.add_argument("--out-align", type=int, default=128,
+                    help="zipf: output slot alignment in bytes (the caller's packing choice)")
     ap.add_argument("--config", default="4k", choices=["4k", "100b", "zipf", "zipf_lane", "open4k", "e2e4k"])
     ap.add_argument("--frames", type=int, default=FRAMES)
     ap.add_argument("--no-cpu-baseline", action="store_true")
@@ -96,7 +99,7 @@ def shard_plan(rank, frames_per_rank, cfg="4k"):
 class Workload:
     """Builds one rank's device-resident batch and the per-step launch."""
 
-    def __init__(self, cfg, frames, rank, dev):
+    def __init__(self, cfg, frames, rank, dev, out_align=128, seg_blocks=64):
         self.cfg = cfg
         self.dev = dev
         key = torch.tensor(list(PRECOM), dtype=torch.uint8, device=dev).view(1, 32)
@@ -137,7 +140,8 @@ class Workload:
             desc = np.zeros(frames, dtype=batch.DESC_DTYPE)
             in_off = np.zeros(frames, dtype=np.uint64)
             in_off[1:] = np.cumsum(lens[:-1])
-            out_len = (lens + np.uint64(33) + np.uint64(15)) // np.uint64(16) * np.uint64(16)
+            al = np.uint64(out_align)
+            out_len = (lens + np.uint64(33) + al - np.uint64(1)) // al * al
             out_off = np.zeros(frames, dtype=np.uint64)
             out_off[1:] = np.cumsum(out_len[:-1])
             desc["in_off"] = in_off
@@ -156,7 +160,7 @@ class Workload:
             self.payload_bytes = in_bytes
             if cfg == "zipf":
                 # long frames split into 64-block segments (one lane each) + Poly1305 combine
-                self.plan = batch.SegmentPlan(desc, open_=False).to(dev)
+                self.plan = batch.SegmentPlan(desc, open_=False, seg_blocks=seg_blocks).to(dev)
                 self.read_bytes = in_bytes + 40 * frames + 16 * self.plan.nseg + 16 * self.plan.ncomb
             else:  # zipf_lane: one lane per frame, longest first
                 order = batch.plan_order(desc)
@@ -318,7 +322,7 @@ def main():
         if rank == 0:
             print(json.dumps(line), flush=True)
         return
-    wl = Workload(args.config, args.frames, rank, dev)
+    wl = Workload(args.config, args.frames, rank, dev, out_align=args.out_align, seg_blocks=args.seg_blocks)
 
     for _ in range(args.warmup):
         wl.step()

@@ -823,34 +823,36 @@ __device__ __forceinline__ u32 ld32(const uint8_t *__restrict__ p)
 
 // Line staging for a wave of segments at arbitrary 16-byte aligned bases.  Like
 // EmitLines, 8 lanes write one 128-byte output line per store instruction, but
-// each lane's base and byte count come from a per-wave LDS table, and stores are
-// clipped to the segment's bytes (ragged frames are packed, nothing is padding).
+// each frame's base and byte count are fetched from its owner lane with
+// ds_bpermute (no LDS table: 8 KiB per wave keeps 5 workgroups per CU), and
+// stores are clipped to the segment's bytes (ragged frames are packed, nothing
+// is padding).  emit/finish/close must be reached by all 64 lanes together:
+// ds_bpermute from an inactive lane returns garbage, not its base.
 struct EmitSegLines {
     uint4 *lds;      // this wave's 64 x 8 chunks
-    u64 *tbase;      // per-lane output base
-    u32 *ttot;       // per-lane byte count; bit 31: leave bytes 16..31 to tag()
     uint8_t *mine;
     u32 lane, total, last_q;
+    u32 tt;          // total | bit 31: leave bytes 16..31 of line 0 to tag()
 
-    __device__ __forceinline__ void init(bool tag_slot)
-    {
-        tbase[lane] = (u64)(uintptr_t)mine;
-        ttot[lane] = total | (tag_slot ? 0x80000000u : 0u);
-    }
+    __device__ __forceinline__ void init(bool tag_slot) { tt = total | (tag_slot ? 0x80000000u : 0u); }
     __device__ __forceinline__ void flush(u32 line)
     {
         const u32 c = lane & 7u;
         const u32 r = lane >> 3;
         const u32 off = 128u * line + 16u * c;
+        const u64 mb = (u64)(uintptr_t)mine;
         asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
 #pragma unroll
         for (u32 j = 0; j < 8; j++) {
             const u32 F = 8u * j + r;
             const uint4 v = lds[F * 8u + (c ^ (F & 7u))];
-            const u32 tt = ttot[F];
-            const u32 tot = tt & 0x7fffffffu;
-            uint8_t *p = reinterpret_cast<uint8_t *>((uintptr_t)tbase[F]) + off;
-            const bool skip = (tt >> 31) && line == 0 && c == 1;
+            const int sel = (int)(F << 2);
+            const u32 blo = (u32)__builtin_amdgcn_ds_bpermute(sel, (int)(u32)mb);
+            const u32 bhi = (u32)__builtin_amdgcn_ds_bpermute(sel, (int)(u32)(mb >> 32));
+            const u32 ft = (u32)__builtin_amdgcn_ds_bpermute(sel, (int)tt);
+            const u32 tot = ft & 0x7fffffffu;
+            uint8_t *p = reinterpret_cast<uint8_t *>((uintptr_t)(((u64)bhi << 32) | blo)) + off;
+            const bool skip = (ft >> 31) && line == 0 && c == 1;
             if (!skip) {
                 if (off + 16u <= tot)
                     *reinterpret_cast<uint4 *>(p) = v;
@@ -907,7 +909,12 @@ __device__ __forceinline__ u32 seal_seg_bytes(u32 mlen, u32 b0, u32 bend)
 // Seal box blocks [b0, b1) of one MESSAGE.  Output chunk q is box block b0 + q
 // at em's base (body + 64*b0).  rec == nullptr: the whole frame, the tag goes
 // to bytes 16..31; otherwise the Poly1305 partial goes to rec.
-template <bool AL, class EM>
+// PAIR (16-byte aligned input): block 2k's window is P[32k-9 .. 32k+7] and
+// block 2k+1's is P[32k+7 .. 32k+23], so each iteration reads payload line k
+// whole (8 back-to-back loads) and seals two blocks from it, carrying the
+// line's last 9 dwords.  Lane-wise 16-byte loads one block apart made L2 fetch
+// most lines twice (2.6x the payload on the Zipf batch).
+template <bool AL, class EM, bool PAIR = false>
 __device__ void seal_segment(const uint8_t *__restrict__ in, u32 n, u32 flags, u64 counter, const u32 key[8], u32 b0,
                              u32 b1, u32 *__restrict__ rec, EM &em)
 {
@@ -915,6 +922,7 @@ __device__ void seal_segment(const uint8_t *__restrict__ in, u32 n, u32 flags, u
     const u32 nblk = (mlen + 63u) >> 6;
     const u32 nfull = mlen >> 6;
     const u32 bend = b1 < nblk ? b1 : nblk;
+    const u32 nch = bend - b0;
     const u64 inlen = n;
     u32 n0, n1;
     counter_nonce(counter, n0, n1);
@@ -922,40 +930,17 @@ __device__ void seal_segment(const uint8_t *__restrict__ in, u32 n, u32 flags, u
     salsa20_block(x, key, n0, n1, 0u, 0u);
     Poly P;
     poly_init(P, x[0], x[1], x[2], x[3], x[4], x[5], x[6], x[7]);
-    u32 carry = b0 == 0 ? (flags << 24) : ld32<AL>(in + 64u * b0 - 36u);  // payload dword P[16*b0 - 9]
     u32 mpoly = 0;
-    for (u32 q = 0; q < bend - b0; q++) {
-        const u32 blk = b0 + q;
+
+    // box block blk from its 17-dword window W = P[16blk-9 .. 16blk+7] (P[-1] = flags << 24)
+    auto block = [&](u32 blk, const u32 *W) {
         salsa20_block(x, key, n0, n1, blk, 0u);
+#pragma unroll
+        for (int k = 0; k < 16; k++)
+            C[k] = funnel(W[k + 1], W[k], 3) ^ x[k];
         if (blk == 0) {
-            V4 a = ld16<AL>(in, inlen);
-            V4 b = ld16<AL>(in + 16, inlen > 16 ? inlen - 16 : 0);
-            u32 W[9] = {carry, a.x, a.y, a.z, a.w, b.x, b.y, b.z, b.w};
-#pragma unroll
-            for (int k = 8; k < 16; k++)
-                C[k] = funnel(W[k - 7], W[k - 8], 3) ^ x[k];
-            carry = b.w;
             C[0] = HDR0; C[1] = HDR1; C[2] = n0; C[3] = n1;
-            C[4] = C[5] = C[6] = C[7] = 0u;
-        } else {
-            const uint8_t *src = in + 64u * blk - 32u;
-            V4 q0, q1, q2, q3;
-            if (blk < nfull) {
-                q0 = ld16f<AL>(src); q1 = ld16f<AL>(src + 16); q2 = ld16f<AL>(src + 32);
-                q3 = ld16<AL>(src + 48, inlen - (64u * blk + 16u));
-            } else {
-                const u64 o = 64u * blk - 32u;
-                q0 = ld16<AL>(src, o < inlen ? inlen - o : 0);
-                q1 = ld16<AL>(src + 16, o + 16 < inlen ? inlen - o - 16 : 0);
-                q2 = ld16<AL>(src + 32, o + 32 < inlen ? inlen - o - 32 : 0);
-                q3 = ld16<AL>(src + 48, o + 48 < inlen ? inlen - o - 48 : 0);
-            }
-            u32 W[17] = {carry, q0.x, q0.y, q0.z, q0.w, q1.x, q1.y, q1.z, q1.w,
-                         q2.x, q2.y, q2.z, q2.w, q3.x, q3.y, q3.z, q3.w};
-#pragma unroll
-            for (int k = 0; k < 16; k++)
-                C[k] = funnel(W[k + 1], W[k], 3) ^ x[k];
-            carry = q3.w;
+            C[4] = C[5] = C[6] = C[7] = 0u;  // tag slot
         }
         if (blk != 0 && blk < nfull) {
             poly_block(P, C[0], C[1], C[2], C[3], 1u);
@@ -977,20 +962,108 @@ __device__ void seal_segment(const uint8_t *__restrict__ in, u32 n, u32 flags, u
                 }
             }
         }
-        em.emit(q, C);
+    };
+
+    if constexpr (PAIR) {
+        static_assert(AL, "PAIR needs 16-byte aligned input");
+        u32 cy[9];  // P[16*b0 - 9 .. 16*b0 - 1]
+        if (b0 == 0) {
+#pragma unroll
+            for (int k = 0; k < 8; k++)
+                cy[k] = 0u;
+            cy[8] = flags << 24;
+        } else {
+            const uint8_t *p = in + 64u * b0 - 48u;
+            V4 a = ld16f<AL>(p), b = ld16f<AL>(p + 16), c = ld16f<AL>(p + 32);
+            cy[0] = a.w; cy[1] = b.x; cy[2] = b.y; cy[3] = b.z; cy[4] = b.w;
+            cy[5] = c.x; cy[6] = c.y; cy[7] = c.z; cy[8] = c.w;
+        }
+        for (u32 q = 0; q < nch; q += 2u) {
+            const u32 blk = b0 + q;
+            const uint8_t *src = in + 64u * blk;
+            const u64 o = 64ull * blk;
+            u32 L[32];
+            if (o + 128u <= inlen) {
+#pragma unroll
+                for (int c = 0; c < 8; c++) {
+                    V4 v = ld16f<AL>(src + 16 * c);
+                    L[4 * c] = v.x; L[4 * c + 1] = v.y; L[4 * c + 2] = v.z; L[4 * c + 3] = v.w;
+                }
+            } else {
+#pragma unroll
+                for (int c = 0; c < 8; c++) {
+                    V4 v = ld16<AL>(src + 16 * c, inlen > o + 16u * c ? inlen - o - 16u * c : 0);
+                    L[4 * c] = v.x; L[4 * c + 1] = v.y; L[4 * c + 2] = v.z; L[4 * c + 3] = v.w;
+                }
+            }
+            u32 W[17];
+#pragma unroll
+            for (int k = 0; k < 9; k++)
+                W[k] = cy[k];
+#pragma unroll
+            for (int k = 0; k < 8; k++)
+                W[9 + k] = L[k];
+            block(blk, W);
+            em.emit(q, C);
+            if (q + 1u < nch) {
+                block(blk + 1u, L + 7);
+                em.emit(q + 1u, C);
+            }
+#pragma unroll
+            for (int k = 0; k < 9; k++)
+                cy[k] = L[23 + k];
+        }
+    } else {
+        u32 carry = b0 == 0 ? (flags << 24) : ld32<AL>(in + 64u * b0 - 36u);  // P[16*b0 - 9]
+        for (u32 q = 0; q < nch; q++) {
+            const u32 blk = b0 + q;
+            u32 W[17];
+            W[0] = carry;
+            if (blk == 0) {
+                V4 a = ld16<AL>(in, inlen);
+                V4 b = ld16<AL>(in + 16, inlen > 16 ? inlen - 16 : 0);
+                // block 0 only uses W[8..16] = P[-1 .. 7]
+                W[8] = carry;
+                W[9] = a.x; W[10] = a.y; W[11] = a.z; W[12] = a.w;
+                W[13] = b.x; W[14] = b.y; W[15] = b.z; W[16] = b.w;
+#pragma unroll
+                for (int k = 1; k < 8; k++)
+                    W[k] = 0u;
+            } else {
+                const uint8_t *src = in + 64u * blk - 32u;
+                V4 q0, q1, q2, q3;
+                if (blk < nfull) {
+                    q0 = ld16f<AL>(src); q1 = ld16f<AL>(src + 16); q2 = ld16f<AL>(src + 32);
+                    q3 = ld16<AL>(src + 48, inlen - (64u * blk + 16u));
+                } else {
+                    const u64 o = 64u * blk - 32u;
+                    q0 = ld16<AL>(src, o < inlen ? inlen - o : 0);
+                    q1 = ld16<AL>(src + 16, o + 16 < inlen ? inlen - o - 16 : 0);
+                    q2 = ld16<AL>(src + 32, o + 32 < inlen ? inlen - o - 32 : 0);
+                    q3 = ld16<AL>(src + 48, o + 48 < inlen ? inlen - o - 48 : 0);
+                }
+                W[1] = q0.x; W[2] = q0.y; W[3] = q0.z; W[4] = q0.w;
+                W[5] = q1.x; W[6] = q1.y; W[7] = q1.z; W[8] = q1.w;
+                W[9] = q2.x; W[10] = q2.y; W[11] = q2.z; W[12] = q2.w;
+                W[13] = q3.x; W[14] = q3.y; W[15] = q3.z; W[16] = q3.w;
+            }
+            block(blk, W);
+            carry = W[16];
+            em.emit(q, C);
+        }
     }
     if (!rec) {
         u32 tag[4];
         poly_finish(P, tag);
         em.tag(tag);
-        em.close(false);
-        return;
     }
-    em.close(false);
-    rec[0] = P.h0; rec[1] = P.h1; rec[2] = P.h2; rec[3] = P.h3; rec[4] = P.h4; rec[5] = mpoly;
-    if (b0 == 0) {
-        rec[8] = P.r0; rec[9] = P.r1; rec[10] = P.r2; rec[11] = P.r3;
-        rec[12] = P.p0; rec[13] = P.p1; rec[14] = P.p2; rec[15] = P.p3;
+    em.close(false);  // convergent: a cooperative flush must see every lane of the wave
+    if (rec) {
+        rec[0] = P.h0; rec[1] = P.h1; rec[2] = P.h2; rec[3] = P.h3; rec[4] = P.h4; rec[5] = mpoly;
+        if (b0 == 0) {
+            rec[8] = P.r0; rec[9] = P.r1; rec[10] = P.r2; rec[11] = P.r3;
+            rec[12] = P.p0; rec[13] = P.p1; rec[14] = P.p2; rec[15] = P.p3;
+        }
     }
 }
 
@@ -1134,15 +1207,16 @@ __device__ u32 open_segment(const uint8_t *__restrict__ in, u32 size, const u32 
         for (int k = 0; k < 8; k++)
             K[k] = X[8 + k];
     }
+    bool bad = false;
     if (!rec) {
         u32 tag[4];
         poly_finish(P, tag);
         V4 tin = ld16<AL>(in + 16, size - 16u);
-        const bool bad = ((tag[0] ^ tin.x) | (tag[1] ^ tin.y) | (tag[2] ^ tin.z) | (tag[3] ^ tin.w)) != 0;
-        em.close(bad);
-        return bad ? CZ_STATUS_CRYPTO : CZ_STATUS_OK;
+        bad = ((tag[0] ^ tin.x) | (tag[1] ^ tin.y) | (tag[2] ^ tin.z) | (tag[3] ^ tin.w)) != 0;
     }
-    em.close(false);
+    em.close(bad);  // convergent: a cooperative flush must see every lane of the wave
+    if (!rec)
+        return bad ? CZ_STATUS_CRYPTO : CZ_STATUS_OK;
     rec[0] = P.h0; rec[1] = P.h1; rec[2] = P.h2; rec[3] = P.h3; rec[4] = P.h4; rec[5] = mpoly;
     if (b0 == 0) {
         rec[6] = flags_out;
@@ -1363,7 +1437,9 @@ __global__ __launch_bounds__(BLOCK) void k_open_uniform(const uint8_t *__restric
 
 
 // ---- segmented (ragged) batches ------------------------------------------
-constexpr u32 SEG_LDS_BYTES = LINE_LDS_BYTES + 64 * 8 + 64 * 4;  // chunks + base/count table per wave
+constexpr u32 SEG_LDS_BYTES = LINE_LDS_BYTES;  // 64 x 128-byte line buffer per wave
+constexpr int SEGMODE_LINES = 1;  // line-staged stores for waves of equal-length segments
+constexpr int SEGMODE_PAIR = 2;   // whole-line input loads (seal)
 
 // A wave takes the line emitter when all 64 lanes hold segments with the same
 // chunk count and 16-byte aligned input/output; otherwise each lane stores directly.
@@ -1378,13 +1454,14 @@ __global__ __launch_bounds__(BLOCK) void k_seal_segments(const cz_frame_desc *__
                                                           const cz_segment *__restrict__ segs, uint32_t nseg,
                                                           const uint8_t *__restrict__ in, uint8_t *__restrict__ out,
                                                           const uint8_t *__restrict__ subkeys,
-                                                          u32 *__restrict__ work, int allow_lines)
+                                                          u32 *__restrict__ work, int mode)
 {
     extern __shared__ uint4 smem[];
     const uint32_t t = blockIdx.x * BLOCK + threadIdx.x;
     const uint32_t wave_first = t & ~63u;
     if (wave_first >= nseg)
         return;
+    const bool allow_lines = mode & SEGMODE_LINES, pair = mode & SEGMODE_PAIR;
     const bool live = t < nseg;
     const cz_segment sg = segs[live ? t : wave_first];
     const cz_frame_desc d = desc[sg.frame];
@@ -1402,17 +1479,24 @@ __global__ __launch_bounds__(BLOCK) void k_seal_segments(const cz_frame_desc *__
     if (allow_lines && wave_lines_ok(wave_first + 64u <= nseg, nch, al)) {
         const u32 lane = threadIdx.x & 63u;
         uint8_t *wl = reinterpret_cast<uint8_t *>(smem) + (threadIdx.x >> 6) * SEG_LDS_BYTES;
-        EmitSegLines em{reinterpret_cast<uint4 *>(wl), reinterpret_cast<u64 *>(wl + LINE_LDS_BYTES),
-                        reinterpret_cast<u32 *>(wl + LINE_LDS_BYTES + 512), dst, lane, total, 0u};
+        EmitSegLines em{reinterpret_cast<uint4 *>(wl), dst, lane, total, 0u, 0u};
         em.init(sg.first_block == 0);
-        seal_segment<true>(src, d.len, d.flags & 0xffu, d.counter, key, sg.first_block, b1, rec, em);
+        if (pair)
+            seal_segment<true, EmitSegLines, true>(src, d.len, d.flags & 0xffu, d.counter, key, sg.first_block, b1,
+                                                   rec, em);
+        else
+            seal_segment<true>(src, d.len, d.flags & 0xffu, d.counter, key, sg.first_block, b1, rec, em);
         return;
     }
     if (!live)
         return;
     if (al) {
         EmitDirect<true> em{dst, total};
-        seal_segment<true>(src, d.len, d.flags & 0xffu, d.counter, key, sg.first_block, b1, rec, em);
+        if (pair)
+            seal_segment<true, EmitDirect<true>, true>(src, d.len, d.flags & 0xffu, d.counter, key, sg.first_block,
+                                                       b1, rec, em);
+        else
+            seal_segment<true>(src, d.len, d.flags & 0xffu, d.counter, key, sg.first_block, b1, rec, em);
     } else {
         EmitDirect<false> em{dst, total};
         seal_segment<false>(src, d.len, d.flags & 0xffu, d.counter, key, sg.first_block, b1, rec, em);
@@ -1442,8 +1526,9 @@ __global__ __launch_bounds__(BLOCK) void k_open_segments(const cz_frame_desc *__
                                                           const uint8_t *__restrict__ in, uint8_t *__restrict__ out,
                                                           const uint8_t *__restrict__ subkeys,
                                                           u32 *__restrict__ work, uint16_t *__restrict__ status,
-                                                          uint64_t *__restrict__ nonces, int allow_lines)
+                                                          uint64_t *__restrict__ nonces, int mode)
 {
+    const bool allow_lines = mode & SEGMODE_LINES;
     extern __shared__ uint4 smem[];
     const uint32_t t = blockIdx.x * BLOCK + threadIdx.x;
     const uint32_t wave_first = t & ~63u;
@@ -1487,8 +1572,7 @@ __global__ __launch_bounds__(BLOCK) void k_open_segments(const cz_frame_desc *__
         __builtin_amdgcn_ballot_w64(early != CZ_STATUS_OK) == 0) {
         const u32 lane = threadIdx.x & 63u;
         uint8_t *wl = reinterpret_cast<uint8_t *>(smem) + (threadIdx.x >> 6) * SEG_LDS_BYTES;
-        EmitSegLines em{reinterpret_cast<uint4 *>(wl), reinterpret_cast<u64 *>(wl + LINE_LDS_BYTES),
-                        reinterpret_cast<u32 *>(wl + LINE_LDS_BYTES + 512), dst, lane, total, 0u};
+        EmitSegLines em{reinterpret_cast<uint4 *>(wl), dst, lane, total, 0u, 0u};
         em.init(false);
         const u32 st = open_segment<true>(src, d.len, key, n0, n1, sg.first_block, b1, rec, fl, em);
         if (!rec)
@@ -1751,7 +1835,7 @@ hipError_t czk_seal_segments(const cz_frame_desc *desc, const cz_segment *segs, 
     if (nseg)
         hipLaunchKernelGGL(k_seal_segments, dim3((nseg + BLOCK - 1) / BLOCK), dim3(BLOCK), WAVES * SEG_LDS_BYTES, s,
                            desc, segs, nseg, (const uint8_t *)in, (uint8_t *)out, (const uint8_t *)subkeys,
-                           (u32 *)work, g_seglines);
+                           (u32 *)work, (g_seglines ? SEGMODE_LINES : 0) | (g_pair ? SEGMODE_PAIR : 0));
     if (ncomb)
         hipLaunchKernelGGL(k_seal_combine, dim3((ncomb + BLOCK - 1) / BLOCK), dim3(BLOCK), 0, s, desc, comb, ncomb,
                            (uint8_t *)out, (const u32 *)work);
@@ -1765,7 +1849,7 @@ hipError_t czk_open_segments(const cz_frame_desc *desc, const cz_segment *segs, 
     if (nseg)
         hipLaunchKernelGGL(k_open_segments, dim3((nseg + BLOCK - 1) / BLOCK), dim3(BLOCK), WAVES * SEG_LDS_BYTES, s,
                            desc, segs, nseg, (const uint8_t *)in, (uint8_t *)out, (const uint8_t *)subkeys,
-                           (u32 *)work, status, nonces, g_seglines);
+                           (u32 *)work, status, nonces, (g_seglines ? SEGMODE_LINES : 0) | (g_pair ? SEGMODE_PAIR : 0));
     if (ncomb)
         hipLaunchKernelGGL(k_open_combine, dim3((ncomb + BLOCK - 1) / BLOCK), dim3(BLOCK), 0, s, desc, comb, ncomb,
                            (const uint8_t *)in, (uint8_t *)out, (const u32 *)work, status);

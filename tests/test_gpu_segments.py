@@ -189,12 +189,13 @@ def test_segments_match_unsplit_kernels(torch_dev, subkeys):
     assert np.array_equal(out_seg, d_out.cpu().numpy())
 
 
-@pytest.mark.parametrize("seglines", [1, 0])
-def test_zipf_seal_open_line_and_direct_stores(torch_dev, subkeys, L, seglines):
-    """Both store paths of the segment kernels (cz_tune "seglines"): a Zipf batch
-    sealed vs the oracle, then opened with tampered and replayed frames mixed in."""
+@pytest.mark.parametrize("seglines,pair", [(1, 1), (1, 0), (0, 1), (0, 0)])
+def test_zipf_seal_open_line_and_direct_stores(torch_dev, subkeys, L, seglines, pair):
+    """Every load/store variant of the segment kernels (cz_tune "seglines", "pair"): a Zipf
+    batch sealed vs the oracle, then opened with tampered and replayed frames mixed in."""
     lib = L.lib()
     old = lib.cz_tune(b"seglines", seglines)
+    old_pair = lib.cz_tune(b"pair", pair)
     try:
         rng = np.random.default_rng(11 + seglines)
         j = np.clip(rng.zipf(1.2, size=3000), 1, 1024)
@@ -231,3 +232,4 @@ def test_zipf_seal_open_line_and_direct_stores(torch_dev, subkeys, L, seglines):
             assert nn[i] == ctr
     finally:
         lib.cz_tune(b"seglines", old)
+        lib.cz_tune(b"pair", old_pair)

@@ -6,16 +6,30 @@ import os
 import sys
 
 root, tag = sys.argv[1], sys.argv[2]
-vals = collections.defaultdict(list)
-dur = []
+vals = collections.defaultdict(lambda: collections.defaultdict(list))
+dur = collections.defaultdict(list)
+
+
+def short(name):
+    return name.split("(")[-2].split("::")[-1] if "(" in name else name
+
+
 for d in sorted(glob.glob(os.path.join(root, tag + "_[0-9]*"))):
     for f in glob.glob(os.path.join(d, "*counter_collection.csv")):
         for r in csv.DictReader(open(f)):
-            vals[r["Counter_Name"]].append(float(r["Counter_Value"]))
-            dur.append((int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) * 1e-9)
-m = {k: sum(v) / len(v) for k, v in vals.items()}
-t = sorted(dur)[len(dur) // 2] if dur else float("nan")
-print(f"kernel (median profiled dispatch) {t*1e3:.3f} ms")
+            k = short(r["Kernel_Name"])
+            vals[k][r["Counter_Name"]].append(float(r["Counter_Value"]))
+            dur[k].append((int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) * 1e-9)
+if not dur:
+    sys.exit("no counter rows")
+# report the dominant kernel (largest total profiled time); list the others
+totals = {k: sum(v) for k, v in dur.items()}
+kern = max(totals, key=totals.get)
+for k in sorted(totals, key=totals.get, reverse=True):
+    print(f"{'*' if k == kern else ' '} {k}: {len(dur[k])} counter rows, median {sorted(dur[k])[len(dur[k]) // 2] * 1e3:.3f} ms")
+m = {c: sum(v) / len(v) for c, v in vals[kern].items()}
+t = sorted(dur[kern])[len(dur[kern]) // 2]
+print(f"kernel {kern} (median profiled dispatch) {t*1e3:.3f} ms")
 for k in sorted(m):
     print(f"  {k:28s} {m[k]:.4e}")
 if "GRBM_GUI_ACTIVE" in m:

@@ -36,14 +36,19 @@ FRAMES = 1 << 20
 def parse():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=20)
-    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--steps", type=int, default=30)
+    ap.add_argument("--warmup", type=int, default=30)
+    ap.add_argument("--ramp-ms", type=float, default=150.0,
+                    help="untimed launches before the W warmup steps until this much GPU time has passed: "
+                         "the clock needs ~100 ms of load to leave its idle state")
     ap.add_argument("--seg-blocks", type=int, default=64, help="zipf: segment length in 64-byte blocks")
     ap.add_argument("--out-align", type=int, default=128,
                     help="zipf: output slot alignment in bytes (the caller's packing choice)")
     ap.add_argument("--config", default="4k", choices=["4k", "100b", "zipf", "zipf_lane", "open4k", "e2e4k"])
     ap.add_argument("--frames", type=int, default=FRAMES)
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-scatter", action="store_true",
+                    help="N>1, 4k: skip the separately timed RCCL scatter -> seal -> gather leg")
     ap.add_argument("--cpu-seconds", type=float, default=10.0, help="target CPU-baseline sample duration")
     return ap.parse_args()
 
@@ -52,10 +57,18 @@ def setup_dist(args):
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    ndev = torch.cuda.device_count()
+    if ndev and local >= ndev:  # rehearsal of N ranks on fewer GPUs (gloo); identity on a full node
+        local %= ndev
     if world > 1:
         import torch.distributed as dist
         torch.cuda.set_device(local)
-        dist.init_process_group("nccl", device_id=torch.device(f"cuda:{local}"))
+        # "nccl" is RCCL on ROCm; CZ_DIST_BACKEND=gloo rehearses N ranks on one GPU
+        backend = os.environ.get("CZ_DIST_BACKEND", "nccl")
+        if backend == "nccl":
+            dist.init_process_group("nccl", device_id=torch.device(f"cuda:{local}"))
+        else:
+            dist.init_process_group(backend)
     else:
         torch.cuda.set_device(0)
     return world, rank, local
@@ -313,6 +326,56 @@ def load_pmc_traffic(cfg):
         return None
 
 
+def scatter_leg(wl, world, rank, dev):
+    """North-star data movement, timed separately: rank 0 holds the whole
+    batch, RCCL-scatters each rank its shard over xGMI, every rank seals its shard, and the
+    bodies are gathered back to rank 0.  Never folded into `value`."""
+    from jeromq_amd import shard
+    import torch.distributed as dist
+    gloo = dist.get_backend() != "nccl"
+    n_in, n_out = wl.d_in.numel(), wl.d_out.numel()
+    sdev = torch.device("cpu") if gloo else dev
+    full_in = full_out = None
+    if rank == 0:
+        full_in = torch.empty(world * n_in, dtype=torch.uint8, device=dev)
+        for r in range(world):
+            batch.fill(full_in[r * n_in:(r + 1) * n_in], shard_plan(r, wl.count, wl.cfg)[1])
+        full_out = torch.empty(world * n_out, dtype=torch.uint8, device=sdev)
+        torch.cuda.synchronize()
+        if gloo:
+            full_in = full_in.cpu()
+    recv = torch.empty(n_in, dtype=torch.uint8, device=sdev)
+    t_sc = shard.timed(lambda: shard.scatter_shards(recv, full_in), world)
+    ok = torch.equal(recv.to(dev), wl.d_in)
+    saved = wl.d_in
+    wl.d_in = recv.to(dev) if gloo else recv
+    t_seal = shard.timed(wl.step, world)
+    wl.d_in = saved
+    send = wl.d_out.cpu() if gloo else wl.d_out
+    t_ga = shard.timed(lambda: shard.gather_shards(send, full_out), world)
+    okt = torch.tensor([1.0 if ok else 0.0], dtype=torch.float64, device="cpu" if gloo else dev)
+    dist.all_reduce(okt, op=dist.ReduceOp.MIN)
+    verified = okt.item() == 1.0
+    if rank == 0:
+        # the last rank's last frame, out of rank 0's gathered buffer, against the oracle
+        sys.path.insert(0, os.path.join(ROOT, "tests"))
+        from cz_testlib import or_curve_encode
+        r, i = world - 1, wl.count - 1
+        base_in, base_out = r * n_in + i * wl.in_stride, r * n_out + i * wl.out_stride
+        p = full_in[base_in:base_in + wl.n].cpu().numpy().tobytes()
+        body = full_out[base_out:base_out + wl.n + 33].cpu().numpy().tobytes()
+        fl = 1 if i % 8 == 0 else 0
+        verified = verified and body == or_curve_encode(p, fl, shard_plan(r, wl.count, wl.cfg)[0] + i, 0, PRECOM)
+    moved_out = (world - 1) * n_in
+    moved_back = (world - 1) * n_out
+    total_payload = world * wl.payload_bytes
+    return {"backend": dist.get_backend(), "scatter_ms": round(t_sc * 1e3, 3), "seal_ms": round(t_seal * 1e3, 3),
+            "gather_ms": round(t_ga * 1e3, 3),
+            "scatter_GBps": round(moved_out / t_sc / 1e9, 2), "gather_GBps": round(moved_back / t_ga / 1e9, 2),
+            "bytes_out_of_rank0": moved_out, "bytes_into_rank0": moved_back,
+            "e2e_GiBps": round(total_payload / (t_sc + t_seal + t_ga) / 2**30, 3), "verified": bool(verified)}
+
+
 def main():
     args = parse()
     world, rank, local = setup_dist(args)
@@ -324,6 +387,13 @@ def main():
         return
     wl = Workload(args.config, args.frames, rank, dev, out_align=args.out_align, seg_blocks=args.seg_blocks)
 
+    ramp = 0
+    t_ramp = time.perf_counter()
+    while (time.perf_counter() - t_ramp) * 1e3 < args.ramp_ms:
+        for _ in range(4):
+            wl.step()
+            ramp += 1
+        torch.cuda.synchronize()
     for _ in range(args.warmup):
         wl.step()
     torch.cuda.synchronize()
@@ -351,6 +421,10 @@ def main():
     achieved = alg_bytes / avg_kernel_s / 1e9
     traffic = load_pmc_traffic(args.config)
 
+    sg = None
+    if world > 1 and args.config == "4k" and not args.no_scatter:
+        sg = scatter_leg(wl, world, rank, dev)
+
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         cpu = cpu_baseline(wl, args.cpu_seconds)
@@ -367,6 +441,7 @@ def main():
             "n_gpus": world,
             "steps": args.steps,
             "warmup": args.warmup,
+            "ramp_steps": ramp,
             "ms_per_step": round(elapsed / args.steps * 1e3, 4),
             "higher_is_better": True,
             "scaling": "weak",
@@ -383,6 +458,8 @@ def main():
                          "alg_bytes_per_launch": alg_bytes},
             "cpu_baseline": cpu,
         }
+        if sg is not None:
+            line["scatter_gather"] = sg
         print(json.dumps(line), flush=True)
     if world > 1:
         import torch.distributed as dist

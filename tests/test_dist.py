@@ -98,3 +98,81 @@ def test_shard_equals_slice_of_global_batch():
     whole = seal(payload, 3)
     parts = [seal(payload[r * F:(r + 1) * F], bench.shard_plan(r, F)[0]) for r in range(2)]
     assert np.array_equal(np.concatenate(parts), whole)
+
+
+def _scatter_worker(rank, world, port, F, n, q):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(world))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        from cz_testlib import DESC_DTYPE, oracle
+        from jeromq_amd import shard
+        first, count = shard.frame_range(rank, world, world * F)
+        full_in = full_out = None
+        if rank == 0:
+            rng = np.random.default_rng(5)
+            full_in = torch.from_numpy(rng.integers(0, 256, size=world * F * n, dtype=np.uint8))
+            full_out = torch.zeros(world * F * (n + 33), dtype=torch.uint8)
+        mine = torch.zeros(count * n, dtype=torch.uint8)
+        shard.scatter_shards(mine, full_in)
+        # seal the shard (oracle stands in for the kernel on CPU) with counters of its range
+        d = np.zeros(count, dtype=DESC_DTYPE)
+        d["in_off"] = np.arange(count) * n
+        d["out_off"] = np.arange(count) * (n + 33)
+        d["len"] = n
+        d["counter"] = 3 + first + np.arange(count)
+        out = np.zeros(count * (n + 33), dtype=np.uint8)
+        p = mine.numpy().copy()
+        oracle().or_seal_batch(d.ctypes.data, count, p.ctypes.data, out.ctypes.data,
+                               np.frombuffer(bytes(range(32)), dtype=np.uint8).copy().ctypes.data, 0, 1)
+        shard.gather_shards(torch.from_numpy(out), full_out)
+        t = shard.timed(lambda: None, world, device_sync=False)
+        q.put((rank, None if full_in is None else (full_in.numpy(), full_out.numpy()), t >= 0))
+    finally:
+        dist.destroy_process_group()
+
+
+def test_rccl_style_scatter_seal_gather_gloo_ws2():
+    """shard.scatter_shards / gather_shards (the north star's scatter/gather leg) with gloo:
+    rank 0's batch, scattered, sealed per shard and gathered back, equals the whole-batch seal."""
+    from cz_testlib import DESC_DTYPE, oracle
+    world, F, n = 2, 16, 100
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_scatter_worker, args=(r, world, port, F, n, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    res = {}
+    for _ in range(world):
+        rank, payload, ok = q.get(timeout=120)
+        res[rank] = (payload, ok)
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    full_in, full_out = res[0][0]
+    d = np.zeros(world * F, dtype=DESC_DTYPE)
+    d["in_off"] = np.arange(world * F) * n
+    d["out_off"] = np.arange(world * F) * (n + 33)
+    d["len"] = n
+    d["counter"] = 3 + np.arange(world * F)
+    want = np.zeros(world * F * (n + 33), dtype=np.uint8)
+    fi = np.ascontiguousarray(full_in)
+    oracle().or_seal_batch(d.ctypes.data, world * F, fi.ctypes.data, want.ctypes.data,
+                           np.frombuffer(bytes(range(32)), dtype=np.uint8).copy().ctypes.data, 0, 1)
+    assert np.array_equal(full_out, want)
+    assert res[0][1] and res[1][1]
+
+
+def test_frame_range_and_byte_balance():
+    from jeromq_amd import shard
+    for total, world in [(10, 3), (1 << 20, 8), (5, 8)]:
+        rs = [shard.frame_range(r, world, total) for r in range(world)]
+        assert sum(c for _, c in rs) == total
+        assert all(rs[i][0] + rs[i][1] == rs[i + 1][0] for i in range(world - 1))
+    rng = np.random.default_rng(42)
+    lens = 64 * np.clip(rng.zipf(1.2, size=100000), 1, 1024)
+    b = shard.balance_by_bytes(lens, 8)
+    assert b[0] == 0 and b[-1] == len(lens) and all(b[i] <= b[i + 1] for i in range(8))
+    work = [int((lens[b[r]:b[r + 1]] + 33).sum()) for r in range(8)]
+    assert max(work) - min(work) <= 2 * (64 * 1024 + 33)   # within ~one max frame of each other
+    assert shard.balance_by_bytes([], 4) == [0, 0, 0, 0, 0]

@@ -66,6 +66,7 @@ extern "C" {
 #define CZ_EHIP (-5)
 #define CZ_ENOMEM (-12)
 #define CZ_EPROTO (-71)
+#define CZ_EMSGSIZE (-90)
 
 /* cz_frame_desc.flags bits (seal: low byte = the MESSAGE flags byte) */
 #define CZ_DESC_CHECK_NONCE 0x100 /* open: enforce nonce > floor (counter or prev frame's nonce) */
@@ -235,14 +236,86 @@ uint64_t cz_mech_peer_nonce(const cz_mech *m);
 #define CZ_ZMTP_INVALID_SEQUENCE 0x10000002
 #define CZ_ZMTP_CRYPTOGRAPHIC 0x11000001
 
+/* ---- 7. ZMTP v2 framing (zmq/io/coder/v2/V2Encoder.java, V2Decoder.java) ----------------
+ * Wire frame = flags byte (MORE 1, LARGE 2, COMMAND 4: V1Protocol/V2Protocol) + size
+ * (1 byte, or BE64 with LARGE when size > 255: V2Encoder.java:31-55) + body. */
+#define CZ_V2_MORE 0x01
+#define CZ_V2_LARGE 0x02
+#define CZ_V2_COMMAND 0x04
+/* header bytes V2Encoder writes before a body of `size` bytes: 2, or 9 when size > 255 */
+uint32_t cz_v2_header_size(uint64_t size);
+/* Host parser with V2Decoder's rules (V2Decoder.java:37-105, Decoder.java:76-98): parses whole
+ * frames from wire[0:len) into frames[] (body offset, size, Msg flags MORE=CZ_MSG_MORE /
+ * COMMAND=CZ_MSG_COMMAND), stopping at cap frames or at an incomplete frame.  *consumed = bytes
+ * of the whole frames.  Returns CZ_OK, or CZ_EPROTO (LARGE size <= 0 as a signed long) /
+ * CZ_EMSGSIZE (size > maxmsgsize >= 0, or > INT32_MAX) at the first bad header; the frames
+ * before it are still reported.  No device needed. */
+typedef struct cz_v2_frame {
+    uint64_t body_off;
+    uint32_t size;
+    uint32_t msg_flags;
+} cz_v2_frame;
+int cz_v2_parse(const uint8_t *wire, uint64_t len, int64_t maxmsgsize, cz_v2_frame *frames, uint32_t cap,
+                uint32_t *nframes, uint64_t *consumed);
+/* Device: one copy per item, any byte alignment.  With CZ_V2_ITEM_HEADER in flags, the V2
+ * header for `size` (wire flags = flags & 0xff, LARGE set by size) is written at dst_off and the
+ * body after it: packing sealed MESSAGE bodies into socket-ready wire streams.  Without it a
+ * plain copy: unpacking received bodies into aligned slots for the open kernels. */
+#define CZ_V2_ITEM_HEADER 0x100
+typedef struct cz_v2_item {
+    uint64_t src_off;
+    uint64_t dst_off;
+    uint32_t size;
+    uint32_t flags;
+} cz_v2_item;
+int cz_v2_copy(const cz_v2_item *d_items, uint32_t count, const void *d_src, void *d_dst, void *stream);
+
+/* ---- 8. batching engine: many CURVE connections, one device batch per flush -----------------
+ * The GPU form of StreamEngine's encode/decode loops (outEvent: pull + mechanism.encode +
+ * V2Encoder up to OUT_BATCH_SIZE, StreamEngine.java:467-535; inEvent: V2Decoder +
+ * mechanism.decode, :379-465, decodeAndPush :1067-1098) across connections: messages of all
+ * connections are sealed in one segmented device batch and packed into per-connection wire
+ * streams; received wire bytes of all connections are parsed, opened in one batch and checked
+ * against each connection's nonce chain.  Payload buffers come from a pinned arena
+ * (ZMQ_MSG_ALLOCATOR, zmq/msg/MsgAllocator.java:5-8).  Not thread-safe: one engine per thread. */
+typedef struct cz_engine cz_engine;
+/* arena_bytes: capacity of the pinned outbound payload arena (messages per flush) */
+int cz_engine_create(cz_engine **e, uint64_t arena_bytes, int device);
+void cz_engine_destroy(cz_engine *e);
+/* returns a connection id >= 0; cn_nonce / cn_peer_nonce as cz_mech_create */
+int cz_engine_add_conn(cz_engine *e, int as_server, const uint8_t precom[32], uint64_t cn_nonce,
+                       uint64_t cn_peer_nonce);
+/* pinned payload buffer inside the arena (no copy at send); NULL when the arena is full */
+void *cz_engine_msg_alloc(cz_engine *e, uint32_t len);
+/* queue one Msg (payload from cz_engine_msg_alloc, or copied into the arena); CZ_ENOMEM when the
+ * arena is full (flush first), CZ_EPROTO when the connection has failed */
+int cz_engine_send(cz_engine *e, int conn, const void *payload, uint32_t len, int msg_flags);
+/* seal every queued Msg on the device and pack each connection's MESSAGE frames, in send order,
+ * into its wire stream (pinned host memory, valid until the next cz_engine_flush_out) */
+int cz_engine_flush_out(cz_engine *e);
+int cz_engine_wire_out(cz_engine *e, int conn, const uint8_t **wire, uint64_t *len);
+/* append bytes received on a connection (partial frames are kept for the next flush) */
+int cz_engine_recv(cz_engine *e, int conn, const void *wire, uint64_t len);
+/* parse, open and sequence-check every whole frame received on every connection */
+int cz_engine_flush_in(cz_engine *e);
+/* decoded messages of the last cz_engine_flush_in (pinned memory, valid until the next one) */
+int cz_engine_msgs_in(cz_engine *e, int conn, uint32_t *count);
+int cz_engine_msg_in(cz_engine *e, int conn, uint32_t i, const uint8_t **payload, uint32_t *len, int *msg_flags);
+/* 0 while the connection is healthy; after a failure CZ_EPROTO / CZ_EMSGSIZE and *event = the
+ * ZMTP protocol-error event the reference raises (0 for a framing error) */
+int cz_engine_conn_error(cz_engine *e, int conn, int *event);
+uint64_t cz_engine_nonce(cz_engine *e, int conn);
+uint64_t cz_engine_peer_nonce(cz_engine *e, int conn);
+
 /* ---- 6. misc -------------------------------------------------------------- */
 const char *cz_last_error(void);
 const char *cz_version(void);
 /* 1 if a HIP device is present and the gfx950 code object loaded */
 int cz_device_ok(void);
 /* Kernel-variant knob for A/B measurement; returns the previous value or CZ_EINVAL.
- *   "pair": 1 = uniform kernels read whole 128-byte input lines per two blocks (default), 0 = per block
- *   "un0":  1 = scalar first Salsa round when the high nonce word is wave-uniform (default), 0 = off */
+ *   "pair": 1 = seal kernels read whole 128-byte input lines per two blocks (default), 0 = per block
+ *   "un0":  1 = scalar first Salsa round when the high nonce word is wave-uniform (default), 0 = off
+ *   "seglines": 1 = line-staged stores in the segment kernels (default), 0 = direct stores */
 int cz_tune(const char *key, int value);
 
 #ifdef __cplusplus

@@ -16,6 +16,7 @@ CZ_EINVAL = -22
 CZ_EHIP = -5
 CZ_ENOMEM = -12
 CZ_EPROTO = -71
+CZ_EMSGSIZE = -90
 
 CZ_STATUS_OK = 0
 CZ_STATUS_CRYPTO = 1
@@ -29,6 +30,11 @@ CZ_MSG_MORE = 0x01
 CZ_MSG_COMMAND = 0x02
 CZ_DESC_CHECK_NONCE = 0x100
 CZ_MESSAGE_OVERHEAD = 33
+
+CZ_V2_MORE = 0x01
+CZ_V2_LARGE = 0x02
+CZ_V2_COMMAND = 0x04
+CZ_V2_ITEM_HEADER = 0x100
 
 CZ_ZMTP_UNEXPECTED_COMMAND = 0x10000001
 CZ_ZMTP_MALFORMED_COMMAND_MESSAGE = 0x10000012
@@ -47,6 +53,18 @@ class cz_frame_desc(ctypes.Structure):
 
 
 assert ctypes.sizeof(cz_frame_desc) == 40
+
+
+class cz_v2_frame(ctypes.Structure):
+    _fields_ = [("body_off", ctypes.c_uint64), ("size", ctypes.c_uint32), ("msg_flags", ctypes.c_uint32)]
+
+
+class cz_v2_item(ctypes.Structure):
+    _fields_ = [("src_off", ctypes.c_uint64), ("dst_off", ctypes.c_uint64), ("size", ctypes.c_uint32),
+                ("flags", ctypes.c_uint32)]
+
+
+assert ctypes.sizeof(cz_v2_frame) == 16 and ctypes.sizeof(cz_v2_item) == 24
 
 _VP = ctypes.c_void_p
 _P = ctypes.c_char_p
@@ -90,6 +108,23 @@ SIGNATURES = {
     "cz_mech_decode_batch": (_I, [_VP, _U32, _VP, _VP, _VP, _VP, _VP, _VP, _VP, ctypes.POINTER(_I)]),
     "cz_mech_nonce": (_U64, [_VP]),
     "cz_mech_peer_nonce": (_U64, [_VP]),
+    "cz_v2_header_size": (_U32, [_U64]),
+    "cz_v2_parse": (_I, [_VP, _U64, ctypes.c_int64, _VP, _U32, ctypes.POINTER(_U32), ctypes.POINTER(_U64)]),
+    "cz_v2_copy": (_I, [_VP, _U32, _VP, _VP, _VP]),
+    "cz_engine_create": (_I, [ctypes.POINTER(_VP), _U64, _I]),
+    "cz_engine_destroy": (None, [_VP]),
+    "cz_engine_add_conn": (_I, [_VP, _I, _VP, _U64, _U64]),
+    "cz_engine_msg_alloc": (_VP, [_VP, _U32]),
+    "cz_engine_send": (_I, [_VP, _I, _VP, _U32, _I]),
+    "cz_engine_flush_out": (_I, [_VP]),
+    "cz_engine_wire_out": (_I, [_VP, _I, ctypes.POINTER(_VP), ctypes.POINTER(_U64)]),
+    "cz_engine_recv": (_I, [_VP, _I, _VP, _U64]),
+    "cz_engine_flush_in": (_I, [_VP]),
+    "cz_engine_msgs_in": (_I, [_VP, _I, ctypes.POINTER(_U32)]),
+    "cz_engine_msg_in": (_I, [_VP, _I, _U32, ctypes.POINTER(_VP), ctypes.POINTER(_U32), ctypes.POINTER(_I)]),
+    "cz_engine_conn_error": (_I, [_VP, _I, ctypes.POINTER(_I)]),
+    "cz_engine_nonce": (_U64, [_VP, _I]),
+    "cz_engine_peer_nonce": (_U64, [_VP, _I]),
     "cz_last_error": (ctypes.c_char_p, []),
     "cz_version": (ctypes.c_char_p, []),
     "cz_device_ok": (_I, []),

@@ -1,0 +1,576 @@
+// cz_engine.cpp -- batching engine: many CURVE connections, one device batch per flush.
+//
+// The reference encrypts one message at a time on each connection's IO thread:
+//   outEvent  (StreamEngine.java:467-535) pulls Msgs, mechanism.encode()s each one
+//             (CurveClientMechanism.java:126-163) and V2Encoder-frames it
+//             (V2Encoder.java:31-55) into an OUT_BATCH_SIZE buffer for the socket;
+//   inEvent   (StreamEngine.java:379-465) V2Decoder-parses the received bytes
+//             (V2Decoder.java:37-105) and decodeAndPush (:1067-1098) mechanism.decode()s
+//             each frame (CurveClientMechanism.java:165-224), tearing the connection down at
+//             the first failure.
+// Here the messages of ALL connections are queued in a pinned arena (the ZMQ_MSG_ALLOCATOR
+// role, zmq/msg/MsgAllocator.java:5-8) and handled per flush with one device batch:
+//   flush_out: descriptors with each connection's next nonces -> H2D -> segmented seal into
+//              128-byte aligned body slots -> k_v2_copy packs every connection's frames, in send
+//              order, behind their V2 headers into one contiguous wire stream per connection ->
+//              D2H into pinned memory, ready for the socket write.
+//   flush_in:  host V2 parse of each connection's received bytes (one header per frame; a
+//              partial frame waits for more bytes) -> H2D of the whole frames -> k_v2_copy unpacks
+//              bodies into aligned slots -> segmented open with the nonce floor chained frame to
+//              frame inside each connection (desc.prev) -> D2H -> per-connection delivery up to the
+//              first failing frame, whose status becomes the connection's error event.
+#include <string.h>
+
+#include <algorithm>
+#include <vector>
+
+#include "cz_internal.h"
+
+using namespace czi;
+
+namespace {
+
+constexpr uint64_t SLOT_ALIGN = 128;  // body / payload slots: line-staged stores, whole-line loads
+constexpr uint32_t SEG_BLOCKS = 64;
+
+uint64_t round_up(uint64_t v, uint64_t a) { return (v + a - 1) / a * a; }
+
+struct Conn {
+    bool server = false;
+    uint32_t tx_key = 0, rx_key = 0;  // subkey table indices
+    uint64_t nonce = 0;               // cnNonce: next MESSAGE nonce to send
+    uint64_t peer_nonce = 0;          // cnPeerNonce: last accepted peer nonce
+    int error = 0;                    // CZ_EPROTO / CZ_EMSGSIZE once torn down
+    int event = 0;                    // ZMTP protocol-error event of the failure
+    std::vector<uint8_t> inbuf;       // received bytes not yet parsed (a partial frame)
+    uint64_t wire_off = 0, wire_len = 0;
+    std::vector<uint32_t> in_msgs;    // indices into Engine::in_msgs of the last flush_in
+};
+
+struct OutMsg {
+    uint32_t conn;
+    uint64_t arena_off;
+    uint32_t len;
+    uint32_t flags;
+};
+
+struct InMsg {
+    uint64_t plain_off;
+    uint32_t len;
+    int flags;
+};
+
+struct Segs {
+    std::vector<cz_segment> seg;
+    std::vector<cz_combine> comb;
+    uint32_t nseg = 0, ncomb = 0, npart = 0;
+};
+
+int plan(const std::vector<cz_frame_desc> &d, int open, Segs &s)
+{
+    s.nseg = s.ncomb = s.npart = 0;
+    cz_plan_segments(d.data(), (uint32_t)d.size(), open, SEG_BLOCKS, nullptr, 0, &s.nseg, nullptr, 0, &s.ncomb,
+                     &s.npart);
+    s.seg.resize(std::max<uint32_t>(s.nseg, 1));
+    s.comb.resize(std::max<uint32_t>(s.ncomb, 1));
+    return cz_plan_segments(d.data(), (uint32_t)d.size(), open, SEG_BLOCKS, s.seg.data(), (uint32_t)s.seg.size(),
+                            &s.nseg, s.comb.data(), (uint32_t)s.comb.size(), &s.ncomb, &s.npart);
+}
+
+}  // namespace
+
+struct cz_engine {
+    int device = 0;
+    hipStream_t stream = nullptr;
+    std::vector<Conn> conns;
+    DevBuf subkeys;  // 32 B per (connection, direction)
+    uint32_t nkeys = 0;
+    // outbound
+    HostBuf arena;
+    uint64_t arena_cap = 0, arena_used = 0;
+    std::vector<OutMsg> pend;
+    HostBuf h_wire;
+    uint64_t wire_total = 0;
+    // inbound
+    HostBuf h_rx, h_plain;
+    std::vector<InMsg> in_msgs;
+    // device staging (grows, never shrinks)
+    DevBuf d_in, d_body, d_wire, d_desc, d_seg, d_comb, d_work, d_items, d_status, d_nonces, d_plain;
+    HostBuf h_status, h_nonces;
+
+    ~cz_engine()
+    {
+        if (stream) {
+            (void)hipSetDevice(device);
+            (void)hipStreamSynchronize(stream);
+            (void)hipStreamDestroy(stream);
+        }
+        for (DevBuf *b : {&subkeys, &d_in, &d_body, &d_wire, &d_desc, &d_seg, &d_comb, &d_work, &d_items, &d_status,
+                          &d_nonces, &d_plain})
+            b->release();
+        for (HostBuf *b : {&arena, &h_wire, &h_rx, &h_plain, &h_status, &h_nonces})
+            b->release();
+    }
+
+    Conn *conn(int c)
+    {
+        if (c < 0 || (size_t)c >= conns.size()) {
+            fail(CZ_EINVAL, "cz_engine: unknown connection %d", c);
+            return nullptr;
+        }
+        return &conns[(size_t)c];
+    }
+
+    // grow the device subkey table to hold `want` keys, keeping its contents
+    hipError_t grow_keys(uint32_t want)
+    {
+        if ((uint64_t)want * 32 <= subkeys.cap)
+            return hipSuccess;
+        void *p = nullptr;
+        const uint64_t bytes = std::max<uint64_t>(4096, (uint64_t)want * 64);
+        hipError_t e = hipMalloc(&p, bytes);
+        if (e != hipSuccess)
+            return e;
+        if (nkeys && (e = hipMemcpyAsync(p, subkeys.ptr, (uint64_t)nkeys * 32, hipMemcpyDeviceToDevice, stream)) !=
+                         hipSuccess)
+            return e;
+        if ((e = hipStreamSynchronize(stream)) != hipSuccess)
+            return e;
+        subkeys.release();
+        subkeys.ptr = p;
+        subkeys.cap = bytes;
+        return hipSuccess;
+    }
+
+    int upload_and_plan(const std::vector<cz_frame_desc> &desc, int open, Segs &s)
+    {
+        int rc = plan(desc, open, s);
+        if (rc != CZ_OK)
+            return rc;
+        hipError_t e;
+        if ((e = d_desc.reserve(desc.size() * sizeof(cz_frame_desc))) != hipSuccess ||
+            (e = d_seg.reserve((uint64_t)s.seg.size() * sizeof(cz_segment))) != hipSuccess ||
+            (e = d_comb.reserve((uint64_t)s.comb.size() * sizeof(cz_combine))) != hipSuccess ||
+            (e = d_work.reserve((uint64_t)std::max<uint32_t>(s.npart, 1) * 64)) != hipSuccess)
+            return hip_fail(e, "cz_engine: hipMalloc");
+        // the host vectors stay alive until the caller synchronises the stream
+        if ((e = hipMemcpyAsync(d_desc.ptr, desc.data(), desc.size() * sizeof(cz_frame_desc), hipMemcpyHostToDevice,
+                                stream)) != hipSuccess ||
+            (e = hipMemcpyAsync(d_seg.ptr, s.seg.data(), (uint64_t)s.nseg * sizeof(cz_segment), hipMemcpyHostToDevice,
+                                stream)) != hipSuccess ||
+            (s.ncomb && (e = hipMemcpyAsync(d_comb.ptr, s.comb.data(), (uint64_t)s.ncomb * sizeof(cz_combine),
+                                            hipMemcpyHostToDevice, stream)) != hipSuccess))
+            return hip_fail(e, "cz_engine: H2D");
+        return CZ_OK;
+    }
+
+    int flush_out()
+    {
+        for (Conn &c : conns)
+            c.wire_off = c.wire_len = 0;
+        wire_total = 0;
+        const uint32_t n = (uint32_t)pend.size();
+        if (n == 0) {
+            arena_used = 0;  // buffers allocated but never sent are released too
+            return CZ_OK;
+        }
+        // wire layout: each connection's frames contiguous, in send order; connections in id order
+        std::vector<uint64_t> conn_bytes(conns.size(), 0);
+        for (const OutMsg &m : pend) {
+            const uint64_t body = (uint64_t)m.len + CZ_MESSAGE_OVERHEAD;
+            conn_bytes[m.conn] += cz_v2_header_size(body) + body;
+        }
+        uint64_t w = 0;
+        for (size_t c = 0; c < conns.size(); c++) {
+            conns[c].wire_off = w;
+            conns[c].wire_len = conn_bytes[c];
+            w += conn_bytes[c];
+        }
+        wire_total = w;
+        std::vector<uint64_t> cursor(conns.size());
+        for (size_t c = 0; c < conns.size(); c++)
+            cursor[c] = conns[c].wire_off;
+        std::vector<cz_frame_desc> desc(n);
+        std::vector<cz_v2_item> items(n);
+        uint64_t slot = 0;
+        for (uint32_t i = 0; i < n; i++) {
+            const OutMsg &m = pend[i];
+            Conn &c = conns[m.conn];
+            const uint64_t body = (uint64_t)m.len + CZ_MESSAGE_OVERHEAD;
+            desc[i] = {m.arena_off, slot, m.len, c.tx_key, c.nonce++, m.flags & 0xffu, -1};
+            items[i] = {slot, cursor[m.conn], (uint32_t)body, (uint32_t)CZ_V2_ITEM_HEADER};
+            cursor[m.conn] += cz_v2_header_size(body) + body;
+            slot += round_up(body, SLOT_ALIGN);
+        }
+        hipError_t e;
+        if ((e = d_in.reserve(std::max<uint64_t>(arena_used, 16))) != hipSuccess ||
+            (e = d_body.reserve(slot)) != hipSuccess || (e = d_wire.reserve(wire_total)) != hipSuccess ||
+            (e = d_items.reserve((uint64_t)n * sizeof(cz_v2_item))) != hipSuccess ||
+            (e = h_wire.reserve(wire_total)) != hipSuccess)
+            return hip_fail(e, "cz_engine: alloc");
+        if ((e = hipMemcpyAsync(d_in.ptr, arena.ptr, arena_used, hipMemcpyHostToDevice, stream)) != hipSuccess ||
+            (e = hipMemcpyAsync(d_items.ptr, items.data(), (uint64_t)n * sizeof(cz_v2_item), hipMemcpyHostToDevice,
+                                stream)) != hipSuccess)
+            return hip_fail(e, "cz_engine: H2D");
+        Segs s;
+        int rc = upload_and_plan(desc, 0, s);
+        if (rc != CZ_OK)
+            return rc;
+        if ((e = czk_seal_segments((const cz_frame_desc *)d_desc.ptr, (const cz_segment *)d_seg.ptr, s.nseg,
+                                   (const cz_combine *)d_comb.ptr, s.ncomb, d_in.ptr, d_body.ptr, subkeys.ptr,
+                                   d_work.ptr, stream)) != hipSuccess ||
+            (e = czk_v2_copy((const cz_v2_item *)d_items.ptr, n, d_body.ptr, d_wire.ptr, stream)) != hipSuccess ||
+            (e = hipMemcpyAsync(h_wire.ptr, d_wire.ptr, wire_total, hipMemcpyDeviceToHost, stream)) != hipSuccess ||
+            (e = hipStreamSynchronize(stream)) != hipSuccess)
+            return hip_fail(e, "cz_engine: flush_out");
+        pend.clear();
+        arena_used = 0;
+        return CZ_OK;
+    }
+
+    static int event_for(uint32_t status, bool server)
+    {
+        switch (status) {
+        case CZ_STATUS_COMMAND: return CZ_ZMTP_UNEXPECTED_COMMAND;
+        case CZ_STATUS_MALFORMED: return CZ_ZMTP_MALFORMED_COMMAND_MESSAGE;
+        case CZ_STATUS_SEQUENCE: return server ? CZ_ZMTP_INVALID_SEQUENCE : CZ_ZMTP_CRYPTOGRAPHIC;
+        default: return CZ_ZMTP_CRYPTOGRAPHIC;
+        }
+    }
+
+    int flush_in()
+    {
+        in_msgs.clear();
+        for (Conn &c : conns)
+            c.in_msgs.clear();
+        // 1. parse every connection's whole frames (V2Decoder), gather them into one staging buffer
+        struct Parsed {
+            uint32_t conn;
+            uint32_t first, count;  // range in frames
+            uint64_t rx_off;        // where the connection's whole-frame bytes start in h_rx
+            uint64_t consumed;
+            int perr;               // framing error after the parsed frames
+        };
+        std::vector<Parsed> parsed;
+        std::vector<cz_v2_frame> frames;
+        uint64_t rx_total = 0;
+        for (size_t ci = 0; ci < conns.size(); ci++) {
+            Conn &c = conns[ci];
+            if (c.error || c.inbuf.empty())
+                continue;
+            // parse in chunks of CH frames (a frame is >= 2 bytes, so sizing by bytes would cost 8x the data)
+            constexpr uint32_t CH = 65536;
+            const size_t base = frames.size();
+            uint64_t consumed = 0;
+            int prc = CZ_OK;
+            for (;;) {
+                const size_t at = frames.size();
+                frames.resize(at + CH);
+                uint32_t nf = 0;
+                uint64_t used = 0;
+                prc = cz_v2_parse(c.inbuf.data() + consumed, c.inbuf.size() - consumed, -1, frames.data() + at, CH,
+                                  &nf, &used);
+                frames.resize(at + nf);
+                for (uint32_t k = 0; k < nf; k++)
+                    frames[at + k].body_off += consumed;
+                consumed += used;
+                if (prc != CZ_OK || nf < CH)
+                    break;
+            }
+            const uint32_t nf = (uint32_t)(frames.size() - base);
+            parsed.push_back({(uint32_t)ci, (uint32_t)base, nf, rx_total, consumed, prc == CZ_OK ? 0 : prc});
+            rx_total += consumed;
+        }
+        const uint32_t n = (uint32_t)frames.size();
+        hipError_t e;
+        if ((e = h_rx.reserve(std::max<uint64_t>(rx_total, 16))) != hipSuccess)
+            return hip_fail(e, "cz_engine: alloc");
+        for (const Parsed &p : parsed)
+            memcpy((uint8_t *)h_rx.ptr + p.rx_off, conns[p.conn].inbuf.data(), p.consumed);
+        // 2. descriptors: bodies unpacked into aligned slots, each connection's frames chained by prev
+        std::vector<cz_frame_desc> desc(n);
+        std::vector<cz_v2_item> items(n);
+        uint64_t bslot = 0, pslot = 0;
+        for (const Parsed &p : parsed) {
+            const Conn &c = conns[p.conn];
+            for (uint32_t k = 0; k < p.count; k++) {
+                const uint32_t i = p.first + k;
+                const cz_v2_frame &f = frames[i];
+                const uint64_t plen = f.size > CZ_MESSAGE_OVERHEAD ? f.size - CZ_MESSAGE_OVERHEAD : 0;
+                items[i] = {p.rx_off + f.body_off, bslot, f.size, 0u};
+                desc[i] = {bslot, pslot, f.size, c.rx_key, c.peer_nonce, CZ_DESC_CHECK_NONCE,
+                           k ? (int32_t)(i - 1) : -1};
+                bslot += round_up(std::max<uint64_t>(f.size, 1), SLOT_ALIGN);
+                pslot += round_up(std::max<uint64_t>(plen, 1), SLOT_ALIGN);
+            }
+        }
+        if (n) {
+            if ((e = d_wire.reserve(rx_total)) != hipSuccess || (e = d_in.reserve(bslot)) != hipSuccess ||
+                (e = d_plain.reserve(pslot)) != hipSuccess ||
+                (e = d_items.reserve((uint64_t)n * sizeof(cz_v2_item))) != hipSuccess ||
+                (e = d_status.reserve((uint64_t)n * 2)) != hipSuccess ||
+                (e = d_nonces.reserve((uint64_t)n * 8)) != hipSuccess ||
+                (e = h_plain.reserve(pslot)) != hipSuccess || (e = h_status.reserve((uint64_t)n * 2)) != hipSuccess ||
+                (e = h_nonces.reserve((uint64_t)n * 8)) != hipSuccess)
+                return hip_fail(e, "cz_engine: alloc");
+            if ((e = hipMemcpyAsync(d_wire.ptr, h_rx.ptr, rx_total, hipMemcpyHostToDevice, stream)) != hipSuccess ||
+                (e = hipMemcpyAsync(d_items.ptr, items.data(), (uint64_t)n * sizeof(cz_v2_item),
+                                    hipMemcpyHostToDevice, stream)) != hipSuccess)
+                return hip_fail(e, "cz_engine: H2D");
+            Segs s;
+            int rc = upload_and_plan(desc, 1, s);
+            if (rc != CZ_OK)
+                return rc;
+            if ((e = czk_v2_copy((const cz_v2_item *)d_items.ptr, n, d_wire.ptr, d_in.ptr, stream)) != hipSuccess ||
+                (e = czk_open_segments((const cz_frame_desc *)d_desc.ptr, (const cz_segment *)d_seg.ptr, s.nseg,
+                                       (const cz_combine *)d_comb.ptr, s.ncomb, d_in.ptr, d_plain.ptr, subkeys.ptr,
+                                       d_work.ptr, (uint16_t *)d_status.ptr, (uint64_t *)d_nonces.ptr, stream)) !=
+                    hipSuccess ||
+                (e = hipMemcpyAsync(h_plain.ptr, d_plain.ptr, pslot, hipMemcpyDeviceToHost, stream)) != hipSuccess ||
+                (e = hipMemcpyAsync(h_status.ptr, d_status.ptr, (uint64_t)n * 2, hipMemcpyDeviceToHost, stream)) !=
+                    hipSuccess ||
+                (e = hipMemcpyAsync(h_nonces.ptr, d_nonces.ptr, (uint64_t)n * 8, hipMemcpyDeviceToHost, stream)) !=
+                    hipSuccess ||
+                (e = hipStreamSynchronize(stream)) != hipSuccess)
+                return hip_fail(e, "cz_engine: flush_in");
+        }
+        // 3. deliver in order per connection, up to the first failure (decodeAndPush returns false)
+        const uint16_t *st = (const uint16_t *)h_status.ptr;
+        const uint64_t *nn = (const uint64_t *)h_nonces.ptr;
+        for (const Parsed &p : parsed) {
+            Conn &c = conns[p.conn];
+            bool failed = false;
+            for (uint32_t k = 0; k < p.count; k++) {
+                const uint32_t i = p.first + k;
+                const uint32_t status = st[i] & 0xffu;
+                if (status != CZ_STATUS_OK) {
+                    c.error = CZ_EPROTO;
+                    c.event = event_for(status, c.server);
+                    failed = true;
+                    break;
+                }
+                c.peer_nonce = nn[i];
+                const uint32_t fl = st[i] >> 8;
+                int mf = 0;
+                if (fl & 0x01)
+                    mf |= CZ_MSG_MORE;
+                if (fl & 0x02)
+                    mf |= CZ_MSG_COMMAND;
+                c.in_msgs.push_back((uint32_t)in_msgs.size());
+                in_msgs.push_back({desc[i].out_off, desc[i].len - CZ_MESSAGE_OVERHEAD, mf});
+            }
+            if (failed) {
+                c.inbuf.clear();
+                continue;
+            }
+            c.inbuf.erase(c.inbuf.begin(), c.inbuf.begin() + (ptrdiff_t)p.consumed);
+            if (p.perr) {  // V2Decoder error after the good frames: StreamEngine error(PROTOCOL)
+                c.error = p.perr;
+                c.event = 0;
+                c.inbuf.clear();
+            }
+        }
+        return CZ_OK;
+    }
+};
+
+extern "C" {
+
+int cz_engine_create(cz_engine **out, uint64_t arena_bytes, int device)
+{
+    if (!out)
+        return fail(CZ_EINVAL, "cz_engine_create: null pointer");
+    *out = nullptr;
+    int n = 0;
+    if (hipGetDeviceCount(&n) != hipSuccess || n == 0)
+        return fail(CZ_EHIP, "no HIP device available (the CURVE path runs only on the GPU)");
+    cz_engine *e = new cz_engine();
+    e->device = device;
+    hipError_t he;
+    if ((he = hipSetDevice(device)) != hipSuccess ||
+        (he = hipStreamCreateWithFlags(&e->stream, hipStreamNonBlocking)) != hipSuccess ||
+        (he = e->arena.reserve(std::max<uint64_t>(arena_bytes, 4096))) != hipSuccess) {
+        delete e;
+        return hip_fail(he, "cz_engine_create");
+    }
+    e->arena_cap = e->arena.cap;
+    *out = e;
+    return CZ_OK;
+}
+
+void cz_engine_destroy(cz_engine *e) { delete e; }
+
+int cz_engine_add_conn(cz_engine *e, int as_server, const uint8_t precom[32], uint64_t cn_nonce,
+                       uint64_t cn_peer_nonce)
+{
+    if (!e || !precom)
+        return fail(CZ_EINVAL, "cz_engine_add_conn: null pointer");
+    hipError_t he;
+    if ((he = hipSetDevice(e->device)) != hipSuccess || (he = e->grow_keys(e->nkeys + 2)) != hipSuccess)
+        return hip_fail(he, "cz_engine_add_conn");
+    void *dk = nullptr;
+    if ((he = hipMalloc(&dk, 32)) != hipSuccess)
+        return hip_fail(he, "hipMalloc");
+    Conn c;
+    c.server = as_server != 0;
+    c.tx_key = e->nkeys;
+    c.rx_key = e->nkeys + 1;
+    c.nonce = cn_nonce;
+    c.peer_nonce = cn_peer_nonce;
+    uint8_t *table = (uint8_t *)e->subkeys.ptr;
+    const int tx = c.server ? CZ_DIR_S2C : CZ_DIR_C2S;
+    const int rx = c.server ? CZ_DIR_C2S : CZ_DIR_S2C;
+    if ((he = hipMemcpyAsync(dk, precom, 32, hipMemcpyHostToDevice, e->stream)) != hipSuccess ||
+        (he = czk_subkeys(dk, table + 32ull * c.tx_key, 1, prefix_for(tx), e->stream)) != hipSuccess ||
+        (he = czk_subkeys(dk, table + 32ull * c.rx_key, 1, prefix_for(rx), e->stream)) != hipSuccess ||
+        (he = hipMemsetAsync(dk, 0, 32, e->stream)) != hipSuccess || (he = hipStreamSynchronize(e->stream)) != hipSuccess) {
+        (void)hipFree(dk);
+        return hip_fail(he, "cz_engine_add_conn: subkeys");
+    }
+    (void)hipFree(dk);
+    e->nkeys += 2;
+    e->conns.push_back(std::move(c));
+    return (int)e->conns.size() - 1;
+}
+
+void *cz_engine_msg_alloc(cz_engine *e, uint32_t len)
+{
+    if (!e)
+        return nullptr;
+    const uint64_t off = round_up(e->arena_used, 16);
+    if (off + len > e->arena_cap)
+        return nullptr;
+    e->arena_used = off + len;
+    return (uint8_t *)e->arena.ptr + off;
+}
+
+int cz_engine_send(cz_engine *e, int conn, const void *payload, uint32_t len, int msg_flags)
+{
+    if (!e || (len && !payload))
+        return fail(CZ_EINVAL, "cz_engine_send: null pointer");
+    Conn *c = e->conn(conn);
+    if (!c)
+        return CZ_EINVAL;
+    if (c->error)
+        return fail(c->error, "cz_engine_send: connection %d has failed", conn);
+    const uint8_t *base = (const uint8_t *)e->arena.ptr;
+    const uint8_t *p = (const uint8_t *)payload;
+    uint64_t off;
+    if (len && p >= base && p + len <= base + e->arena_used) {
+        off = (uint64_t)(p - base);  // allocated by cz_engine_msg_alloc: no copy
+    } else {
+        uint8_t *dst = (uint8_t *)cz_engine_msg_alloc(e, len);
+        if (!dst)
+            return fail(CZ_ENOMEM, "cz_engine_send: arena full (%llu bytes), flush first",
+                        (unsigned long long)e->arena_cap);
+        if (len)
+            memcpy(dst, p, len);
+        off = (uint64_t)(dst - base);
+    }
+    uint32_t fl = 0;
+    if (msg_flags & CZ_MSG_MORE)
+        fl |= 0x01;
+    if (msg_flags & CZ_MSG_COMMAND)
+        fl |= 0x02;
+    e->pend.push_back({(uint32_t)conn, off, len, fl});
+    return CZ_OK;
+}
+
+int cz_engine_flush_out(cz_engine *e)
+{
+    if (!e)
+        return fail(CZ_EINVAL, "cz_engine_flush_out: null engine");
+    hipError_t he = hipSetDevice(e->device);
+    if (he != hipSuccess)
+        return hip_fail(he, "hipSetDevice");
+    return e->flush_out();
+}
+
+int cz_engine_wire_out(cz_engine *e, int conn, const uint8_t **wire, uint64_t *len)
+{
+    if (!e || !wire || !len)
+        return fail(CZ_EINVAL, "cz_engine_wire_out: null pointer");
+    Conn *c = e->conn(conn);
+    if (!c)
+        return CZ_EINVAL;
+    *wire = (const uint8_t *)e->h_wire.ptr + c->wire_off;
+    *len = c->wire_len;
+    return CZ_OK;
+}
+
+int cz_engine_recv(cz_engine *e, int conn, const void *wire, uint64_t len)
+{
+    if (!e || (len && !wire))
+        return fail(CZ_EINVAL, "cz_engine_recv: null pointer");
+    Conn *c = e->conn(conn);
+    if (!c)
+        return CZ_EINVAL;
+    if (c->error)
+        return fail(c->error, "cz_engine_recv: connection %d has failed", conn);
+    const uint8_t *p = (const uint8_t *)wire;
+    c->inbuf.insert(c->inbuf.end(), p, p + len);
+    return CZ_OK;
+}
+
+int cz_engine_flush_in(cz_engine *e)
+{
+    if (!e)
+        return fail(CZ_EINVAL, "cz_engine_flush_in: null engine");
+    hipError_t he = hipSetDevice(e->device);
+    if (he != hipSuccess)
+        return hip_fail(he, "hipSetDevice");
+    return e->flush_in();
+}
+
+int cz_engine_msgs_in(cz_engine *e, int conn, uint32_t *count)
+{
+    if (!e || !count)
+        return fail(CZ_EINVAL, "cz_engine_msgs_in: null pointer");
+    Conn *c = e->conn(conn);
+    if (!c)
+        return CZ_EINVAL;
+    *count = (uint32_t)c->in_msgs.size();
+    return CZ_OK;
+}
+
+int cz_engine_msg_in(cz_engine *e, int conn, uint32_t i, const uint8_t **payload, uint32_t *len, int *msg_flags)
+{
+    if (!e || !payload || !len || !msg_flags)
+        return fail(CZ_EINVAL, "cz_engine_msg_in: null pointer");
+    Conn *c = e->conn(conn);
+    if (!c)
+        return CZ_EINVAL;
+    if (i >= c->in_msgs.size())
+        return fail(CZ_EINVAL, "cz_engine_msg_in: index %u out of range", i);
+    const InMsg &m = e->in_msgs[c->in_msgs[i]];
+    *payload = (const uint8_t *)e->h_plain.ptr + m.plain_off;
+    *len = m.len;
+    *msg_flags = m.flags;
+    return CZ_OK;
+}
+
+int cz_engine_conn_error(cz_engine *e, int conn, int *event)
+{
+    if (!e)
+        return fail(CZ_EINVAL, "cz_engine_conn_error: null engine");
+    Conn *c = e->conn(conn);
+    if (!c)
+        return CZ_EINVAL;
+    if (event)
+        *event = c->event;
+    return c->error;
+}
+
+uint64_t cz_engine_nonce(cz_engine *e, int conn)
+{
+    Conn *c = e ? e->conn(conn) : nullptr;
+    return c ? c->nonce : 0;
+}
+
+uint64_t cz_engine_peer_nonce(cz_engine *e, int conn)
+{
+    Conn *c = e ? e->conn(conn) : nullptr;
+    return c ? c->peer_nonce : 0;
+}
+
+}  // extern "C"

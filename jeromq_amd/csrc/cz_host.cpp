@@ -28,10 +28,6 @@ hipError_t czk_box_nacl(const void *, void *, uint32_t, const void *, uint64_t, 
 hipError_t czk_subkeys(const void *, void *, uint32_t, const uint8_t *, hipStream_t);
 hipError_t czk_fill(void *, uint64_t, uint64_t, hipStream_t);
 int czk_tune(const char *, int);
-hipError_t czk_seal_segments(const cz_frame_desc *, const cz_segment *, uint32_t, const cz_combine *, uint32_t,
-                             const void *, void *, const void *, void *, hipStream_t);
-hipError_t czk_open_segments(const cz_frame_desc *, const cz_segment *, uint32_t, const cz_combine *, uint32_t,
-                             const void *, void *, const void *, void *, uint16_t *, uint64_t *, hipStream_t);
 }
 
 namespace czi {

@@ -12,6 +12,11 @@ hipError_t czk_seal_desc(const cz_frame_desc *, const uint32_t *, uint32_t, cons
 hipError_t czk_open_desc(const cz_frame_desc *, const uint32_t *, uint32_t, const void *, void *, const void *,
                          uint16_t *, uint64_t *, hipStream_t);
 hipError_t czk_subkeys(const void *, void *, uint32_t, const uint8_t *, hipStream_t);
+hipError_t czk_seal_segments(const cz_frame_desc *, const cz_segment *, uint32_t, const cz_combine *, uint32_t,
+                             const void *, void *, const void *, void *, hipStream_t);
+hipError_t czk_open_segments(const cz_frame_desc *, const cz_segment *, uint32_t, const cz_combine *, uint32_t,
+                             const void *, void *, const void *, void *, uint16_t *, uint64_t *, hipStream_t);
+hipError_t czk_v2_copy(const cz_v2_item *, uint32_t, const void *, void *, hipStream_t);
 }
 
 namespace czi {

@@ -1626,6 +1626,84 @@ __global__ __launch_bounds__(BLOCK) void k_open_combine(const cz_frame_desc *__r
     }
 }
 
+
+// ---- ZMTP v2 framing (V2Encoder / V2Decoder) -------------------------------
+// One wave per item copies `size` bytes between arbitrary byte offsets: lane w
+// owns 16-byte aligned destination word w (lanes coalesce on consecutive words),
+// reads the 5 source dwords that cover it with clamped aligned loads and
+// funnels them by the item's constant byte shift; partially covered edge words
+// are stored byte by byte (adjacent items and headers own the other bytes).
+// With CZ_V2_ITEM_HEADER, the V2Encoder header (V2Encoder.java:31-55: flags byte
+// with LARGE for size > 255, then a 1-byte size or a BE64 size) is written at
+// dst_off and the body after it.
+__device__ __forceinline__ u32 ld_dw_clamped(const uint8_t *__restrict__ base, intptr_t lo, intptr_t hi, intptr_t a)
+{
+    a = a < lo ? lo : (a > hi ? hi : a);
+    return *reinterpret_cast<const u32 *>(base + a);
+}
+
+__global__ __launch_bounds__(BLOCK) void k_v2_copy(const cz_v2_item *__restrict__ items, uint32_t count,
+                                                    const uint8_t *__restrict__ src, uint8_t *__restrict__ dst)
+{
+    const uint32_t wave = __builtin_amdgcn_readfirstlane((blockIdx.x * BLOCK + threadIdx.x) >> 6);
+    const u32 lane = threadIdx.x & 63u;
+    if (wave >= count)
+        return;
+    const cz_v2_item it = items[wave];
+    uint64_t d = it.dst_off;
+    if (it.flags & CZ_V2_ITEM_HEADER) {
+        const bool large = it.size > 255u;
+        const u32 h = large ? 9u : 2u;
+        if (lane < h) {
+            u32 b;
+            if (lane == 0)
+                b = (it.flags & 0xffu & ~(u32)CZ_V2_LARGE) | (large ? (u32)CZ_V2_LARGE : 0u);
+            else if (!large)
+                b = it.size;
+            else
+                b = (u32)((uint64_t)it.size >> (8u * (8u - lane)));  // BE64, Wire.putUInt64
+            dst[d + lane] = (uint8_t)b;
+        }
+        d += h;
+    }
+    const u32 n = it.size;
+    if (n == 0)
+        return;
+    const uintptr_t t0 = (uintptr_t)(dst + d);
+    const uintptr_t s0 = (uintptr_t)(src + it.src_off);
+    const uintptr_t a0 = t0 & ~(uintptr_t)15;
+    const uintptr_t tend = t0 + n;
+    const uint64_t nw = (tend - a0 + 15u) >> 4;
+    // source byte for destination byte x is s0 + (x - t0): constant shift r within aligned dwords
+    const intptr_t sdelta = (intptr_t)s0 - (intptr_t)t0;
+    const u32 r = (u32)(sdelta & 3);
+    const uint8_t *sbase = reinterpret_cast<const uint8_t *>(s0 & ~(uintptr_t)3);
+    const intptr_t lo = 0, hi = (intptr_t)(((s0 + n - 1u) & ~(uintptr_t)3) - (s0 & ~(uintptr_t)3));
+    for (uint64_t w = lane; w < nw; w += 64u) {
+        const uintptr_t D = a0 + 16u * w;
+        // aligned source dword holding the source byte of destination byte D
+        const intptr_t j0 = (intptr_t)((D + sdelta) & ~(uintptr_t)3) - (intptr_t)(s0 & ~(uintptr_t)3);
+        u32 S[5];
+#pragma unroll
+        for (int k = 0; k < 5; k++)
+            S[k] = ld_dw_clamped(sbase, lo, hi, j0 + 4 * k);
+        u32 o[4];
+#pragma unroll
+        for (int k = 0; k < 4; k++)
+            o[k] = r ? funnel(S[k + 1], S[k], r) : S[k];
+        uint8_t *p = reinterpret_cast<uint8_t *>(D);
+        if (D >= t0 && D + 16u <= tend) {
+            *reinterpret_cast<uint4 *>(p) = make_uint4(o[0], o[1], o[2], o[3]);
+        } else {
+            for (u32 b = 0; b < 16u; b++) {
+                const uintptr_t x = D + b;
+                if (x >= t0 && x < tend)
+                    p[b] = (uint8_t)(o[b >> 2] >> (8u * (b & 3u)));
+            }
+        }
+    }
+}
+
 // NaCl-layout single frame (jnacl crypto_box_afternm / crypto_box_open_afternm drop-in).
 // params: subkey (32 B device), counter = BE64(n[16:24]).
 __global__ __launch_bounds__(64) void k_box_nacl(const uint8_t *__restrict__ in, uint8_t *__restrict__ out,
@@ -1853,6 +1931,16 @@ hipError_t czk_open_segments(const cz_frame_desc *desc, const cz_segment *segs, 
     if (ncomb)
         hipLaunchKernelGGL(k_open_combine, dim3((ncomb + BLOCK - 1) / BLOCK), dim3(BLOCK), 0, s, desc, comb, ncomb,
                            (const uint8_t *)in, (uint8_t *)out, (const u32 *)work, status);
+    return hipGetLastError();
+}
+
+hipError_t czk_v2_copy(const cz_v2_item *items, uint32_t count, const void *src, void *dst, hipStream_t s)
+{
+    if (count == 0)
+        return hipSuccess;
+    const uint32_t per_block = BLOCK / 64;
+    hipLaunchKernelGGL(k_v2_copy, dim3((count + per_block - 1) / per_block), dim3(BLOCK), 0, s, items, count,
+                       (const uint8_t *)src, (uint8_t *)dst);
     return hipGetLastError();
 }
 

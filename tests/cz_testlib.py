@@ -128,3 +128,59 @@ def or_curve_decode(body, from_server, k):
 DESC_DTYPE = np.dtype([("in_off", "<u8"), ("out_off", "<u8"), ("len", "<u4"), ("key_idx", "<u4"),
                        ("counter", "<u8"), ("flags", "<u4"), ("prev", "<i4")])
 assert DESC_DTYPE.itemsize == 40
+
+
+# ---- ZMTP v2 framing restated (test infrastructure) -------------------------------------
+def v2_encode(body, msg_flags=0):
+    """V2Encoder.messageReady + sizeReady (zmq/io/coder/v2/V2Encoder.java:24-62): flags byte
+    (MORE 1, LARGE 2 when size > 255, COMMAND 4), the size as 1 byte or BE64 (Wire.putUInt64),
+    then the body.  msg_flags uses Msg's bits (MORE 1, COMMAND 2)."""
+    f = (1 if msg_flags & 1 else 0) | (4 if msg_flags & 2 else 0)
+    body = bytes(body)
+    if len(body) > 255:
+        return bytes([f | 2]) + len(body).to_bytes(8, "big") + body
+    return bytes([f, len(body)]) + body
+
+
+class V2DecoderModel:
+    """The V2Decoder state machine (V2Decoder.java:37-105) with Decoder.sizeReady's checks
+    (zmq/io/coder/Decoder.java:76-98), fed arbitrary chunks like socket reads.
+    Decoded messages are (offset of the body in the whole stream, size, Msg flags)."""
+
+    def __init__(self, maxmsgsize=-1):
+        self.maxmsgsize = maxmsgsize
+        self.state, self.need, self.tmp = "flags", 1, b""
+        self.pos = 0                 # bytes of the stream consumed so far
+        self.msgs, self.error = [], None
+        self.flags = self.size = self.body_off = 0
+
+    def feed(self, data):
+        for b in bytes(data):
+            if self.error:
+                return
+            self.tmp += bytes([b])
+            self.pos += 1
+            if len(self.tmp) < self.need:
+                continue
+            if self.state == "flags":
+                first = self.tmp[0]
+                self.flags = (1 if first & 1 else 0) | (2 if first & 4 else 0)
+                self.state, self.need = ("size8", 8) if first & 2 else ("size1", 1)
+                self.tmp = b""
+            elif self.state in ("size1", "size8"):
+                size = int.from_bytes(self.tmp, "big")
+                if self.state == "size8" and (size == 0 or size >= 1 << 63):   # long `size <= 0`
+                    self.error = "EPROTO"
+                    return
+                if (self.maxmsgsize >= 0 and size > self.maxmsgsize) or size > 0x7fffffff:
+                    self.error = "EMSGSIZE"
+                    return
+                self.size, self.body_off, self.tmp = size, self.pos, b""
+                if size == 0:
+                    self.msgs.append((self.body_off, 0, self.flags))
+                    self.state, self.need = "flags", 1
+                else:
+                    self.state, self.need = "body", size
+            else:
+                self.msgs.append((self.body_off, self.size, self.flags))
+                self.state, self.need, self.tmp = "flags", 1, b""

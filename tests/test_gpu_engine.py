@@ -1,0 +1,182 @@
+"""GPU: the ZMTP v2 pack/unpack kernel and the batching engine (cz_engine_*).
+
+The engine's outbound wire stream for each connection must equal, byte for byte,
+what JeroMQ would write: V2Encoder framing (restated in cz_testlib.v2_encode) of
+each MESSAGE body sealed by the oracle with that connection's nonces.  Inbound,
+the engine must deliver exactly the payloads and flags, keep partial frames
+across reads, and tear a connection down at its first bad frame with the
+reference's event while other connections carry on.
+"""
+import numpy as np
+import pytest
+
+from cz_testlib import load_golden, or_curve_encode, splitmix_bytes, v2_encode
+
+pytestmark = pytest.mark.gpu
+
+G = load_golden()
+PRECOM = bytes.fromhex(G["keys"]["precom"])
+
+
+@pytest.fixture(scope="module")
+def torch_dev():
+    import torch
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    return torch, torch.device("cuda:0")
+
+
+@pytest.fixture(scope="module")
+def L():
+    from jeromq_amd import _lib
+    return _lib
+
+
+def _precom(i):
+    """distinct per-connection keys; connection 0 uses the golden key"""
+    return PRECOM if i == 0 else splitmix_bytes(32, 4242 + i)
+
+
+@pytest.mark.parametrize("header", [False, True])
+def test_v2_copy_any_alignment(torch_dev, header):
+    torch, dev = torch_dev
+    from jeromq_amd import wire
+    rng = np.random.default_rng(3 + header)
+    n = 300
+    sizes = rng.choice([0, 1, 3, 15, 16, 17, 63, 64, 255, 256, 300, 1000, 4129, 70000], size=n)
+    src = rng.integers(0, 256, size=int(sizes.sum()) + 64 * n + 4096, dtype=np.uint8)
+    items = np.zeros(n, dtype=wire.V2_ITEM_DTYPE)
+    so = rng.integers(0, 7)
+    do = int(rng.integers(0, 13))
+    want = np.full(int(sizes.sum()) + 16 * n + 4096, 0xEE, dtype=np.uint8)
+    for i, s in enumerate(sizes):
+        s = int(s)
+        so += int(rng.integers(0, 5))
+        fl = int(rng.integers(0, 8)) if header else 0
+        items[i] = (so, do, s, (0x100 | fl) if header else 0)
+        body = src[so:so + s].tobytes()
+        out = v2_encode(body, 0) if header else body
+        if header:
+            f = (fl & ~2) | (2 if s > 255 else 0)
+            out = bytes([f]) + out[1:]
+        want[do:do + len(out)] = np.frombuffer(out, dtype=np.uint8)
+        so += s
+        do += len(out)   # contiguous output, like a wire stream
+    d_items = torch.from_numpy(items.view(np.uint8).copy()).to(dev)
+    d_src = torch.from_numpy(src).to(dev)
+    d_dst = torch.full((len(want),), 0xEE, dtype=torch.uint8, device=dev)
+    wire.copy(d_items, d_src, d_dst)
+    torch.cuda.synchronize()
+    assert np.array_equal(d_dst.cpu().numpy(), want)
+
+
+def _oracle_wire(msgs, precom, from_server, nonce0):
+    return b"".join(v2_encode(or_curve_encode(p, fl, nonce0 + k, from_server, precom))
+                    for k, (p, fl) in enumerate(msgs))
+
+
+def _messages(rng, n, seed):
+    sizes = rng.choice([0, 1, 31, 100, 222, 223, 4096, 5000, 65536], size=n)
+    return [(splitmix_bytes(int(s), seed + k), int(rng.integers(0, 4))) for k, s in enumerate(sizes)]
+
+
+def test_engine_roundtrip_many_connections(torch_dev, L):
+    from jeromq_amd.engine import CurveBatchEngine
+    rng = np.random.default_rng(1)
+    ncon = 5
+    cli = CurveBatchEngine(arena_bytes=8 << 20)
+    srv = CurveBatchEngine(arena_bytes=8 << 20)
+    cc = [cli.add_connection(_precom(i), as_server=False) for i in range(ncon)]
+    sc = [srv.add_connection(_precom(i), as_server=True) for i in range(ncon)]
+    sent = {i: _messages(rng, 12 + 3 * i, 100 * i) for i in range(ncon)}
+    # interleave sends across connections, as IO threads would
+    order = [(i, k) for i in range(ncon) for k in range(len(sent[i]))]
+    rng.shuffle(order)
+    order.sort(key=lambda t: t[1])   # keep each connection's own order
+    for i, k in order:
+        p, fl = sent[i][k]
+        assert cli.send(cc[i], p, more=bool(fl & 1), command=bool(fl & 2)) == 0
+    cli.flush_out()
+    wires = {}
+    for i in range(ncon):
+        w = cli.wire_out(cc[i])
+        assert w == _oracle_wire(sent[i], _precom(i), 0, 3), f"connection {i}"
+        wires[i] = w
+        assert cli.nonce(cc[i]) == 3 + len(sent[i])
+    # server side: feed each connection's stream in random pieces, flushing in between
+    got = {i: [] for i in range(ncon)}
+    pos = {i: 0 for i in range(ncon)}
+    while any(pos[i] < len(wires[i]) for i in range(ncon)):
+        for i in range(ncon):
+            if pos[i] < len(wires[i]):
+                step = int(rng.integers(1, 40000))
+                srv.recv(sc[i], wires[i][pos[i]:pos[i] + step])
+                pos[i] += step
+        srv.flush_in()
+        for i in range(ncon):
+            got[i] += srv.messages_in(sc[i])
+    for i in range(ncon):
+        assert srv.error(sc[i]) == (0, 0)
+        assert [(p, fl) for p, fl in got[i]] == sent[i]
+        assert srv.peer_nonce(sc[i]) == 3 + len(sent[i]) - 1
+
+
+def test_engine_server_to_client_and_msg_alloc(torch_dev, L):
+    from jeromq_amd.engine import CurveBatchEngine
+    srv = CurveBatchEngine(arena_bytes=1 << 20)
+    cli = CurveBatchEngine(arena_bytes=1 << 20)
+    s = srv.add_connection(PRECOM, as_server=True)
+    c = cli.add_connection(PRECOM, as_server=False)
+    msgs = [(bytes([7]) * n, 1 if n % 2 else 0) for n in (5, 300, 4096)]
+    for p, fl in msgs:
+        buf = srv.msg_alloc(len(p))           # pinned arena buffer: sent without a copy
+        buf[:] = p
+        assert srv.send(s, buf, more=bool(fl)) == 0
+    srv.flush_out()
+    w = srv.wire_out(s)
+    assert w == _oracle_wire(msgs, PRECOM, 1, 2)
+    cli.recv(c, w)
+    cli.flush_in()
+    assert cli.messages_in(c) == msgs
+
+
+def test_engine_failures_tear_down_one_connection(torch_dev, L):
+    from jeromq_amd.engine import CurveBatchEngine
+    rng = np.random.default_rng(5)
+    cli = CurveBatchEngine()
+    srv = CurveBatchEngine()
+    cc = [cli.add_connection(_precom(i)) for i in range(4)]
+    sc = [srv.add_connection(_precom(i), as_server=True) for i in range(4)]
+    sent = {i: _messages(rng, 6, 900 + i) for i in range(4)}
+    for i in range(4):
+        for p, fl in sent[i]:
+            cli.send(cc[i], p, more=bool(fl & 1), command=bool(fl & 2))
+    cli.flush_out()
+    w = {i: bytearray(cli.wire_out(cc[i])) for i in range(4)}
+    # conn 1: flip a ciphertext byte in frame 3; conn 2: replay frame 1 after frame 2;
+    # conn 3: a LARGE header with size 0 after frame 4 (framing error)
+    from jeromq_amd import wire as v2
+    frames = {i: v2.parse(bytes(w[i]))[0] for i in range(4)}
+    f3 = frames[1][3]
+    w[1][int(f3["body_off"]) + int(f3["size"]) - 1] ^= 1
+    f1, f2 = frames[2][1], frames[2][2]
+    hdr1 = v2.header_size(int(f1["size"]))
+    frame1 = bytes(w[2][int(f1["body_off"]) - hdr1:int(f1["body_off"]) + int(f1["size"])])
+    end2 = int(f2["body_off"]) + int(f2["size"])
+    w[2] = w[2][:end2] + frame1 + w[2][end2:]
+    f4 = frames[3][4]
+    end4 = int(f4["body_off"]) + int(f4["size"])
+    w[3] = w[3][:end4] + bytes([2]) + bytes(8) + w[3][end4:]
+    for i in range(4):
+        srv.recv(sc[i], bytes(w[i]))
+    srv.flush_in()
+    assert srv.error(sc[0]) == (0, 0) and srv.messages_in(sc[0]) == sent[0]
+    assert srv.error(sc[1]) == (L.CZ_EPROTO, L.CZ_ZMTP_CRYPTOGRAPHIC)
+    assert srv.messages_in(sc[1]) == sent[1][:3]
+    assert srv.error(sc[2]) == (L.CZ_EPROTO, L.CZ_ZMTP_INVALID_SEQUENCE)   # server-side replay event
+    assert srv.messages_in(sc[2]) == sent[2][:3]
+    assert srv.error(sc[3]) == (L.CZ_EPROTO, 0)                            # V2Decoder EPROTO, no event
+    assert srv.messages_in(sc[3]) == sent[3][:5]
+    # a torn-down connection refuses further traffic; the others keep working
+    assert srv.recv(sc[1], b"\x00\x01x") == L.CZ_EPROTO
+    assert srv.send(sc[0], b"still fine") == 0

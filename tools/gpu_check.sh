@@ -13,9 +13,9 @@ echo "== smoke"
 timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke()" > gpurun_out/smoke.log 2>&1 || { tail gpurun_out/smoke.log; exit 3; }
 tail -2 gpurun_out/smoke.log
 echo "== bench 4k"
-timeout -k 10 300 python bench.py --steps 10 --warmup 2 > gpurun_out/bench_4k.log 2>&1 || { tail gpurun_out/bench_4k.log; exit 4; }
+timeout -k 10 300 python bench.py > gpurun_out/bench_4k.log 2>&1 || { tail gpurun_out/bench_4k.log; exit 4; }
 tail -1 gpurun_out/bench_4k.log
-for cfg in 100b zipf open4k e2e4k; do
+for cfg in 100b zipf zipf_lane open4k e2e4k; do
   echo "== bench $cfg"
   timeout -k 10 300 python bench.py --steps 10 --warmup 2 --config $cfg --no-cpu-baseline > gpurun_out/bench_$cfg.log 2>&1 || { tail gpurun_out/bench_$cfg.log; exit 5; }
   tail -1 gpurun_out/bench_$cfg.log
@@ -23,4 +23,6 @@ done
 echo "== rocprofv3 kernel trace"
 timeout -k 10 300 rocprofv3 --kernel-trace --stats -T --output-format csv -d gpurun_out/prof_4k -o run -- python3 bench.py --steps 5 --warmup 1 --no-cpu-baseline > gpurun_out/prof_4k.log 2>&1 || { tail gpurun_out/prof_4k.log; exit 6; }
 find gpurun_out/prof_4k -name "*stats*" | head
+echo "== rocprofv3 kernel trace (zipf)"
+timeout -k 10 300 rocprofv3 --kernel-trace --stats -T --output-format csv -d gpurun_out/prof_zipf -o run -- python3 bench.py --steps 5 --warmup 1 --config zipf --no-cpu-baseline > gpurun_out/prof_zipf.log 2>&1 || { tail gpurun_out/prof_zipf.log; exit 7; }
 exit 0

@@ -15,6 +15,7 @@ frames (counters offset by rank * 2^20): no collective on the timed path ("weak"
 Rank 0 prints ONE JSON line.  `value` = payload GiB/s over all ranks.
 """
 import argparse
+import ctypes
 import json
 import os
 import sys
@@ -44,7 +45,7 @@ def parse():
     ap.add_argument("--seg-blocks", type=int, default=64, help="zipf: segment length in 64-byte blocks")
     ap.add_argument("--out-align", type=int, default=128,
                     help="zipf: output slot alignment in bytes (the caller's packing choice)")
-    ap.add_argument("--config", default="4k", choices=["4k", "100b", "zipf", "zipf_lane", "open4k", "e2e4k"])
+    ap.add_argument("--config", default="4k", choices=["4k", "100b", "zipf", "zipf_lane", "open4k", "e2e4k", "engine"])
     ap.add_argument("--frames", type=int, default=FRAMES)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-scatter", action="store_true",
@@ -312,6 +313,59 @@ def e2e_host(args, dev):
                                    f"{chunk}-frame chunks", "frames": frames}}
 
 
+def engine_host(args, dev):
+    """Batching engine end-to-end (cz_engine_*): 1024 connections x 256 MESSAGEs of 4 KiB.
+    flush_out = descriptors + H2D + segmented seal + V2 pack + D2H into per-connection wire
+    streams; flush_in = V2 parse + H2D + unpack + open + D2H + per-connection delivery.
+    Wall clock per flush; the Python send/recv loops are timed apart (ctypes overhead)."""
+    from jeromq_amd.engine import CurveBatchEngine
+    sys.path.insert(0, os.path.join(ROOT, "tests"))
+    from cz_testlib import or_curve_encode, v2_encode
+    nconn, per, n = 1024, 256, 4096
+    total = nconn * per * n
+    cli = CurveBatchEngine(arena_bytes=total + (1 << 20))
+    srv = CurveBatchEngine(arena_bytes=1 << 20)
+    keys = [bytes((PRECOM[j] + c) & 0xff for j in range(32)) for c in range(nconn)]
+    cc = [cli.add_connection(keys[c]) for c in range(nconn)]
+    sc = [srv.add_connection(keys[c], as_server=True) for c in range(nconn)]
+    payload = np.random.default_rng(7).integers(0, 256, size=per * n, dtype=np.uint8).tobytes()
+    res = {}
+    for rep in range(3):          # first round warms allocations and clocks
+        t0 = time.perf_counter()
+        for c in range(nconn):
+            for k in range(per):
+                buf = cli.msg_alloc(n)
+                ctypes.memmove(buf, payload[k * n:(k + 1) * n], n)
+                cli.send(cc[c], buf, more=(k % 8 == 0))
+        t_send = time.perf_counter() - t0
+        t0 = time.perf_counter()
+        cli.flush_out()
+        t_out = time.perf_counter() - t0
+        wires = [cli.wire_out(cc[c]) for c in range(nconn)]
+        t0 = time.perf_counter()
+        for c in range(nconn):
+            srv.recv(sc[c], wires[c])
+        t_recv = time.perf_counter() - t0
+        t0 = time.perf_counter()
+        srv.flush_in()
+        t_in = time.perf_counter() - t0
+        res = {"send_loop_s": t_send, "flush_out_s": t_out, "recv_loop_s": t_recv, "flush_in_s": t_in}
+    # parity spot checks: connection 5's first frame on the wire, connection 9's last message in
+    nonce0 = 3 + 2 * per   # third round
+    first = v2_encode(or_curve_encode(payload[:n], 1, nonce0, 0, keys[5]))
+    ok = wires[5][:len(first)] == first
+    got = srv.messages_in(sc[9])
+    ok = ok and len(got) == per and got[-1][0] == payload[(per - 1) * n:per * n]
+    ok = ok and all(srv.error(sc[c])[0] == 0 for c in range(nconn))
+    msgs = nconn * per
+    return {"metric": "CURVE batching engine end-to-end GiB/s (pinned host, 1024 connections, ZMTP v2 wire)",
+            "value": round(total / res["flush_out_s"] / 2**30, 3), "unit": "GiB/s", "n_gpus": 1,
+            "open_GiBps": round(total / res["flush_in_s"] / 2**30, 3),
+            "msgs_per_s_out": round(msgs / res["flush_out_s"], 1), "msgs_per_s_in": round(msgs / res["flush_in_s"], 1),
+            "timings_s": {k: round(v, 4) for k, v in res.items()}, "verified": bool(ok),
+            "config": {"workload": f"{nconn} connections x {per} x {n} B MESSAGEs per flush", "frames": msgs}}
+
+
 def load_pmc_traffic(cfg):
     """HBM bytes per launch from the committed rocprofv3 PMC summary, if one exists for this config."""
     path = os.path.join(ROOT, "profiles", "pmc_traffic.json")
@@ -380,8 +434,8 @@ def main():
     args = parse()
     world, rank, local = setup_dist(args)
     dev = torch.device(f"cuda:{local}")
-    if args.config == "e2e4k":
-        line = e2e_host(args, dev)
+    if args.config in ("e2e4k", "engine"):
+        line = e2e_host(args, dev) if args.config == "e2e4k" else engine_host(args, dev)
         if rank == 0:
             print(json.dumps(line), flush=True)
         return

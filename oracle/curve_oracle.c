@@ -441,3 +441,205 @@ void or_seal_batch(const or_frame_desc *d, uint64_t count, const uint8_t *in, ui
     for (int t = 0; t < nthreads; t++)
         pthread_join(th[t], NULL);
 }
+
+/* ------------------------------------------------------------------------------------
+ * X25519 and crypto_box (the CURVE handshake's key agreement).
+ *   Curve.beforenm  -> jnacl crypto_box_beforenm   Curve.java:124-127
+ *   Curve.keypair   -> jnacl crypto_box_keypair    Curve.java:100-115
+ *   Curve.box/open  -> jnacl crypto_box[_open]     Curve.java:149-193
+ * Restated from RFC 7748 section 5 (Montgomery ladder, a24 = 121665, clamped scalar,
+ * u masked to 255 bits) in radix 2^51 with 128-bit products -- the device uses radix
+ * 2^25.5 with 32x32->64 multiply-adds, so again no arithmetic is shared.
+ * beforenm(k, pk, sk) = HSalsa20(X25519(sk, pk), 0^16): NaCl crypto_box_beforenm.
+ * ---------------------------------------------------------------------------------- */
+typedef uint64_t or_fe[5];
+typedef unsigned __int128 or_u128;
+static const uint64_t OR_M51 = (1ull << 51) - 1;
+
+static void or_fe_frombytes(or_fe h, const uint8_t s[32])
+{
+    uint64_t w[4];
+    for (int i = 0; i < 4; i++) {
+        w[i] = 0;
+        for (int b = 7; b >= 0; b--)
+            w[i] = (w[i] << 8) | s[8 * i + b];
+    }
+    h[0] = w[0] & OR_M51;
+    h[1] = ((w[0] >> 51) | (w[1] << 13)) & OR_M51;
+    h[2] = ((w[1] >> 38) | (w[2] << 26)) & OR_M51;
+    h[3] = ((w[2] >> 25) | (w[3] << 39)) & OR_M51;
+    h[4] = (w[3] >> 12) & OR_M51; /* bit 255 masked (RFC 7748 section 5) */
+}
+
+static void or_fe_carry(or_fe h)
+{
+    for (int r = 0; r < 2; r++) {
+        uint64_t c;
+        for (int i = 0; i < 4; i++) {
+            c = h[i] >> 51;
+            h[i] &= OR_M51;
+            h[i + 1] += c;
+        }
+        c = h[4] >> 51;
+        h[4] &= OR_M51;
+        h[0] += 19 * c;
+    }
+}
+
+static void or_fe_tobytes(uint8_t s[32], const or_fe f)
+{
+    or_fe h;
+    memcpy(h, f, sizeof(or_fe));
+    or_fe_carry(h);
+    /* h < 2^255 + small: subtract p if h >= p */
+    uint64_t q = (h[0] + 19) >> 51;
+    q = (h[1] + q) >> 51;
+    q = (h[2] + q) >> 51;
+    q = (h[3] + q) >> 51;
+    q = (h[4] + q) >> 51;
+    h[0] += 19 * q;
+    for (int i = 0; i < 4; i++) {
+        h[i + 1] += h[i] >> 51;
+        h[i] &= OR_M51;
+    }
+    h[4] &= OR_M51;
+    uint64_t w[4] = {h[0] | (h[1] << 51), (h[1] >> 13) | (h[2] << 38), (h[2] >> 26) | (h[3] << 25),
+                     (h[3] >> 39) | (h[4] << 12)};
+    for (int i = 0; i < 4; i++)
+        for (int b = 0; b < 8; b++)
+            s[8 * i + b] = (uint8_t)(w[i] >> (8 * b));
+}
+
+static void or_fe_add(or_fe h, const or_fe f, const or_fe g)
+{
+    for (int i = 0; i < 5; i++)
+        h[i] = f[i] + g[i];
+}
+
+/* h = f - g + 4p (limbs stay positive for carried inputs) */
+static void or_fe_sub(or_fe h, const or_fe f, const or_fe g)
+{
+    static const uint64_t P4[5] = {4 * (OR_M51 - 18), 4 * OR_M51, 4 * OR_M51, 4 * OR_M51, 4 * OR_M51};
+    for (int i = 0; i < 5; i++)
+        h[i] = f[i] + P4[i] - g[i];
+    or_fe_carry(h);
+}
+
+static void or_fe_mul(or_fe h, const or_fe f, const or_fe g)
+{
+    or_u128 t[5] = {0, 0, 0, 0, 0};
+    for (int i = 0; i < 5; i++)
+        for (int j = 0; j < 5; j++) {
+            or_u128 p = (or_u128)f[i] * g[j];
+            if (i + j < 5)
+                t[i + j] += p;
+            else
+                t[i + j - 5] += p * 19;
+        }
+    or_u128 c = 0;
+    for (int i = 0; i < 5; i++) {
+        t[i] += c;
+        h[i] = (uint64_t)t[i] & OR_M51;
+        c = t[i] >> 51;
+    }
+    h[0] += (uint64_t)c * 19;
+    or_fe_carry(h);
+}
+
+static void or_fe_mul_small(or_fe h, const or_fe f, uint64_t k)
+{
+    or_u128 c = 0;
+    for (int i = 0; i < 5; i++) {
+        or_u128 t = (or_u128)f[i] * k + c;
+        h[i] = (uint64_t)t & OR_M51;
+        c = t >> 51;
+    }
+    h[0] += (uint64_t)c * 19;
+    or_fe_carry(h);
+}
+
+static void or_fe_pow(or_fe h, const or_fe f, const uint8_t e[32]) /* square-and-multiply, e little-endian */
+{
+    or_fe r = {1, 0, 0, 0, 0};
+    for (int bit = 255; bit >= 0; bit--) {
+        or_fe_mul(r, r, r);
+        if ((e[bit >> 3] >> (bit & 7)) & 1)
+            or_fe_mul(r, r, f);
+    }
+    memcpy(h, r, sizeof(or_fe));
+}
+
+static void or_fe_cswap(or_fe a, or_fe b, uint64_t swap)
+{
+    const uint64_t m = 0 - swap;
+    for (int i = 0; i < 5; i++) {
+        uint64_t t = m & (a[i] ^ b[i]);
+        a[i] ^= t;
+        b[i] ^= t;
+    }
+}
+
+/* X25519(k, u) per RFC 7748 section 5 */
+void or_x25519(uint8_t out[32], const uint8_t scalar[32], const uint8_t u[32])
+{
+    uint8_t k[32];
+    memcpy(k, scalar, 32);
+    k[0] &= 248;
+    k[31] &= 127;
+    k[31] |= 64;
+    or_fe x1, x2 = {1, 0, 0, 0, 0}, z2 = {0, 0, 0, 0, 0}, x3, z3 = {1, 0, 0, 0, 0};
+    or_fe_frombytes(x1, u);
+    memcpy(x3, x1, sizeof(or_fe));
+    uint64_t swap = 0;
+    for (int t = 254; t >= 0; t--) {
+        const uint64_t kt = (k[t >> 3] >> (t & 7)) & 1;
+        swap ^= kt;
+        or_fe_cswap(x2, x3, swap);
+        or_fe_cswap(z2, z3, swap);
+        swap = kt;
+        or_fe A, AA, B, BB, E, C, D, DA, CB, t0, t1;
+        or_fe_add(A, x2, z2);
+        or_fe_mul(AA, A, A);
+        or_fe_sub(B, x2, z2);
+        or_fe_mul(BB, B, B);
+        or_fe_sub(E, AA, BB);
+        or_fe_add(C, x3, z3);
+        or_fe_sub(D, x3, z3);
+        or_fe_mul(DA, D, A);
+        or_fe_mul(CB, C, B);
+        or_fe_add(t0, DA, CB);
+        or_fe_mul(x3, t0, t0);
+        or_fe_sub(t1, DA, CB);
+        or_fe_mul(t1, t1, t1);
+        or_fe_mul(z3, x1, t1);
+        or_fe_mul(x2, AA, BB);
+        or_fe_mul_small(t0, E, 121665);
+        or_fe_add(t0, AA, t0);
+        or_fe_mul(z2, E, t0);
+    }
+    or_fe_cswap(x2, x3, swap);
+    or_fe_cswap(z2, z3, swap);
+    /* z2^(p-2), p - 2 = 2^255 - 21 */
+    static const uint8_t PM2[32] = {0xeb, 0xff, 0xff, 0xff, 0xff, 0xff, 0xff, 0xff, 0xff, 0xff, 0xff,
+                                    0xff, 0xff, 0xff, 0xff, 0xff, 0xff, 0xff, 0xff, 0xff, 0xff, 0xff,
+                                    0xff, 0xff, 0xff, 0xff, 0xff, 0xff, 0xff, 0xff, 0xff, 0x7f};
+    or_fe zi, r;
+    or_fe_pow(zi, z2, PM2);
+    or_fe_mul(r, x2, zi);
+    or_fe_tobytes(out, r);
+}
+
+void or_scalarmult_base(uint8_t pk[32], const uint8_t sk[32])
+{
+    uint8_t nine[32] = {9};
+    or_x25519(pk, sk, nine);
+}
+
+/* NaCl crypto_box_beforenm: k = HSalsa20(X25519(sk, pk), 0^16) */
+void or_box_beforenm(uint8_t k[32], const uint8_t pk[32], const uint8_t sk[32])
+{
+    uint8_t s[32];
+    static const uint8_t zero[16] = {0};
+    or_x25519(s, sk, pk);
+    or_hsalsa20(k, zero, s);
+}

@@ -71,6 +71,9 @@ def oracle():
     lib.or_splitmix64.argtypes = [U64, U64]
     lib.or_splitmix64.restype = U64
     lib.or_fill.argtypes = [P, U64, U64]
+    lib.or_x25519.argtypes = [P, P, P]
+    lib.or_scalarmult_base.argtypes = [P, P]
+    lib.or_box_beforenm.argtypes = [P, P, P]
     lib.or_seal_batch.argtypes = [ctypes.c_void_p, U64, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p,
                                   ctypes.c_int, ctypes.c_int]
     _ORACLE = lib
@@ -184,3 +187,29 @@ class V2DecoderModel:
             else:
                 self.msgs.append((self.body_off, self.size, self.flags))
                 self.state, self.need, self.tmp = "flags", 1, b""
+
+
+def load_x25519_golden():
+    with open(os.path.join(os.path.dirname(GOLDEN), "x25519_vectors.json")) as f:
+        return json.load(f)
+
+
+def or_x25519(k, u):
+    out = ctypes.create_string_buffer(32)
+    oracle().or_x25519(out, bytes(k), bytes(u))
+    return out.raw
+
+
+def or_beforenm(pk, sk):
+    out = ctypes.create_string_buffer(32)
+    oracle().or_box_beforenm(out, bytes(pk), bytes(sk))
+    return out.raw
+
+
+def or_box(m, n24, pk, sk):
+    """NaCl crypto_box = secretbox under beforenm(pk, sk); m without the 32 zero bytes"""
+    k = or_beforenm(pk, sk)
+    mm = bytes(32) + bytes(m)
+    c = ctypes.create_string_buffer(len(mm))
+    assert oracle().or_secretbox(c, mm, len(mm), bytes(n24), k) == 0
+    return c.raw

@@ -307,6 +307,23 @@ int cz_engine_conn_error(cz_engine *e, int conn, int *event);
 uint64_t cz_engine_nonce(cz_engine *e, int conn);
 uint64_t cz_engine_peer_nonce(cz_engine *e, int conn);
 
+/* ---- 9. handshake public-key calls (Curve.java:84-193 -> jnacl) --------------------------
+ * jnacl int contract (0 / -1).  X25519 per RFC 7748 on the device; box / box_open are
+ * beforenm + the section-1 afternm calls.  The secret key of cz_box_keypair comes from the OS
+ * CSPRNG (getrandom), the public key from X25519(sk, 9) on the device. */
+int cz_scalarmult(uint8_t q[32], const uint8_t n[32], const uint8_t p[32]);             /* crypto_scalarmult */
+int cz_box_keypair(uint8_t pk[32], uint8_t sk[32]);                                      /* Curve.java:100-115 */
+int cz_box_beforenm(uint8_t k[32], const uint8_t pk[32], const uint8_t sk[32]);          /* Curve.java:124-127 */
+int cz_box(uint8_t *c, const uint8_t *m, uint64_t mlen, const uint8_t n[24], const uint8_t pk[32],
+           const uint8_t sk[32]);                                                        /* Curve.java:183-193 */
+int cz_box_open(uint8_t *m, const uint8_t *c, uint64_t clen, const uint8_t n[24], const uint8_t pk[32],
+                const uint8_t sk[32]);                                                   /* Curve.java:149-157 */
+/* Device batches for connection churn (one lane per key agreement, 32-byte records):
+ * out[i] = X25519(scalars[i], points[i]) (points NULL = base point 9);
+ * k[i] = beforenm(pk[i], sk[i]) = HSalsa20(X25519(sk[i], pk[i]), 0^16). */
+int cz_x25519_batch(const void *d_scalars, const void *d_points, void *d_out, uint32_t count, void *stream);
+int cz_beforenm_batch(const void *d_pk, const void *d_sk, void *d_k, uint32_t count, void *stream);
+
 /* ---- 6. misc -------------------------------------------------------------- */
 const char *cz_last_error(void);
 const char *cz_version(void);

@@ -125,6 +125,13 @@ SIGNATURES = {
     "cz_engine_conn_error": (_I, [_VP, _I, ctypes.POINTER(_I)]),
     "cz_engine_nonce": (_U64, [_VP, _I]),
     "cz_engine_peer_nonce": (_U64, [_VP, _I]),
+    "cz_scalarmult": (_I, [_VP, _VP, _VP]),
+    "cz_box_keypair": (_I, [_VP, _VP]),
+    "cz_box_beforenm": (_I, [_VP, _VP, _VP]),
+    "cz_box": (_I, [_VP, _VP, _U64, _VP, _VP, _VP]),
+    "cz_box_open": (_I, [_VP, _VP, _U64, _VP, _VP, _VP]),
+    "cz_x25519_batch": (_I, [_VP, _VP, _VP, _U32, _VP]),
+    "cz_beforenm_batch": (_I, [_VP, _VP, _VP, _U32, _VP]),
     "cz_last_error": (ctypes.c_char_p, []),
     "cz_version": (ctypes.c_char_p, []),
     "cz_device_ok": (_I, []),

@@ -1,10 +1,12 @@
-"""Mirror of zmq.io.mechanism.curve.Curve (jeromq-core/src/main/java/zmq/io/mechanism/curve/Curve.java)
-for the per-message calls, backed by the gfx950 kernels through the C-ABI.
+"""Mirror of zmq.io.mechanism.curve.Curve (jeromq-core/src/main/java/zmq/io/mechanism/curve/Curve.java),
+backed by the gfx950 kernels through the C-ABI.
 
 Same names, argument meaning and int return contract (0 success / -1 failure) as
 Curve.afternm (Curve.java:129-137), Curve.openAfternm (:139-147),
-Curve.secretbox (:159-167) and Curve.secretboxOpen (:169-177).  Each call is one
-device launch; use jeromq_amd.batch for throughput.
+Curve.secretbox (:159-167), Curve.secretboxOpen (:169-177), and the handshake calls
+Curve.keypair (:100-115), Curve.beforenm (:124-127), Curve.box (:183-193) and
+Curve.open (:149-157).  Each call is one device launch; use jeromq_amd.batch (and
+cz_beforenm_batch) for throughput.
 """
 import ctypes
 
@@ -49,6 +51,27 @@ class Curve:
         c = _inbuf(box, length, "box")
         return _lib.lib().cz_secretbox_open(_outbuf(plaintext, length), c, length, bytes(nonce), bytes(key))
 
+    # ---- handshake calls (X25519 on the device) ----
+    def keypair(self):
+        """[public, secret] as 32-byte bytes (Curve.keypair, Curve.java:100-115)."""
+        pk, sk = ctypes.create_string_buffer(32), ctypes.create_string_buffer(32)
+        rc = _lib.lib().cz_box_keypair(pk, sk)
+        assert rc == 0, _lib.last_error()
+        return [pk.raw, sk.raw]
+
+    def beforenm(self, outSharedKey, publicKey, secretKey):
+        return _lib.lib().cz_box_beforenm(_outbuf(outSharedKey, 32), bytes(publicKey), bytes(secretKey))
+
+    def box(self, ciphertext, plaintext, length, nonce, publicKey, secretKey):
+        m = _inbuf(plaintext, length, "plaintext")
+        return _lib.lib().cz_box(_outbuf(ciphertext, length), m, length, bytes(nonce), bytes(publicKey),
+                                 bytes(secretKey))
+
+    def open(self, plaintext, messagebox, length, nonce, publicKey, secretKey):
+        c = _inbuf(messagebox, length, "messagebox")
+        return _lib.lib().cz_box_open(_outbuf(plaintext, length), c, length, bytes(nonce), bytes(publicKey),
+                                      bytes(secretKey))
+
     # snake_case aliases
     open_afternm = openAfternm
     secretbox_open = secretboxOpen
@@ -58,4 +81,12 @@ def subkey(precom, direction):
     """HSalsa20(precom, "CurveZMQMESSAGE{C|S}") -- the per-connection-direction Salsa20 key."""
     out = ctypes.create_string_buffer(32)
     _lib.check(_lib.lib().cz_subkey(out, bytes(precom), direction), "cz_subkey")
+    return out.raw
+
+
+def scalarmult(n, p):
+    """X25519(n, p) (crypto_scalarmult, RFC 7748), computed on the device."""
+    out = ctypes.create_string_buffer(32)
+    if _lib.lib().cz_scalarmult(out, bytes(n), bytes(p)) != 0:
+        raise _lib.CzError("cz_scalarmult failed: " + _lib.last_error())
     return out.raw

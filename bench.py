@@ -45,7 +45,7 @@ def parse():
     ap.add_argument("--seg-blocks", type=int, default=64, help="zipf: segment length in 64-byte blocks")
     ap.add_argument("--out-align", type=int, default=128,
                     help="zipf: output slot alignment in bytes (the caller's packing choice)")
-    ap.add_argument("--config", default="4k", choices=["4k", "100b", "zipf", "zipf_lane", "open4k", "e2e4k", "engine"])
+    ap.add_argument("--config", default="4k", choices=["4k", "100b", "zipf", "zipf_lane", "open4k", "e2e4k", "engine", "beforenm"])
     ap.add_argument("--frames", type=int, default=FRAMES)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-scatter", action="store_true",
@@ -366,6 +366,49 @@ def engine_host(args, dev):
             "config": {"workload": f"{nconn} connections x {per} x {n} B MESSAGEs per flush", "frames": msgs}}
 
 
+def beforenm_bench(args, dev):
+    """Handshake key agreement: cz_beforenm_batch over 2^18 random key
+    pairs per launch (connection churn), timed with HIP events; oracle on 1 host thread beside it."""
+    from jeromq_amd import _lib
+    sys.path.insert(0, os.path.join(ROOT, "tests"))
+    from cz_testlib import or_beforenm
+    n = 1 << 18
+    g = torch.Generator(device="cpu").manual_seed(7)
+    pk = torch.randint(0, 256, (32 * n,), dtype=torch.uint8, generator=g).to(dev)
+    sk = torch.randint(0, 256, (32 * n,), dtype=torch.uint8, generator=g).to(dev)
+    k = torch.empty(32 * n, dtype=torch.uint8, device=dev)
+    L = _lib.lib()
+    s = torch.cuda.current_stream()
+
+    def step():
+        _lib.check(L.cz_beforenm_batch(pk.data_ptr(), sk.data_ptr(), k.data_ptr(), n, ctypes.c_void_p(s.cuda_stream)),
+                   "cz_beforenm_batch")
+    for _ in range(max(args.warmup, 2)):
+        step()
+    torch.cuda.synchronize()
+    evs = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(args.steps)]
+    for a, b in evs:
+        a.record(s)
+        step()
+        b.record(s)
+    torch.cuda.synchronize()
+    ms = float(np.median([a.elapsed_time(b) for a, b in evs]))
+    hp, hs, hk = pk.cpu().numpy().tobytes(), sk.cpu().numpy().tobytes(), k.cpu().numpy().tobytes()
+    ok = all(hk[32 * i:32 * i + 32] == or_beforenm(hp[32 * i:32 * i + 32], hs[32 * i:32 * i + 32])
+             for i in (0, 1, n // 2, n - 1))
+    t0 = time.perf_counter()
+    cnt = 0
+    while time.perf_counter() - t0 < 2.0:
+        or_beforenm(hp[:32], hs[:32])
+        cnt += 1
+    cpu_rate = cnt / (time.perf_counter() - t0)
+    return {"metric": "CURVE handshake beforenm (X25519 + HSalsa20) per second, device batch",
+            "value": round(n / (ms / 1e3), 1), "unit": "ops/s", "n_gpus": 1, "steps": args.steps,
+            "kernel_ms": round(ms, 4), "batch": n, "verified": bool(ok),
+            "cpu_baseline": {"value": round(cpu_rate, 1), "unit": "ops/s", "cores": 1, "kind": "port",
+                             "sample": "oracle/curve_oracle.c or_box_beforenm (radix 2^51), 2 s on 1 thread"}}
+
+
 def load_pmc_traffic(cfg):
     """HBM bytes per launch from the committed rocprofv3 PMC summary, if one exists for this config."""
     path = os.path.join(ROOT, "profiles", "pmc_traffic.json")
@@ -434,8 +477,8 @@ def main():
     args = parse()
     world, rank, local = setup_dist(args)
     dev = torch.device(f"cuda:{local}")
-    if args.config in ("e2e4k", "engine"):
-        line = e2e_host(args, dev) if args.config == "e2e4k" else engine_host(args, dev)
+    if args.config in ("e2e4k", "engine", "beforenm"):
+        line = {"e2e4k": e2e_host, "engine": engine_host, "beforenm": beforenm_bench}[args.config](args, dev)
         if rank == 0:
             print(json.dumps(line), flush=True)
         return

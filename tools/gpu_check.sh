@@ -15,7 +15,7 @@ tail -2 gpurun_out/smoke.log
 echo "== bench 4k"
 timeout -k 10 300 python bench.py > gpurun_out/bench_4k.log 2>&1 || { tail gpurun_out/bench_4k.log; exit 4; }
 tail -1 gpurun_out/bench_4k.log
-for cfg in 100b zipf zipf_lane open4k e2e4k engine; do
+for cfg in 100b zipf zipf_lane open4k e2e4k engine beforenm; do
   echo "== bench $cfg"
   timeout -k 10 300 python bench.py --steps 10 --warmup 2 --config $cfg --no-cpu-baseline > gpurun_out/bench_$cfg.log 2>&1 || { tail gpurun_out/bench_$cfg.log; exit 5; }
   tail -1 gpurun_out/bench_$cfg.log

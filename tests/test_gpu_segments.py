@@ -233,3 +233,68 @@ def test_zipf_seal_open_line_and_direct_stores(torch_dev, subkeys, L, seglines, 
     finally:
         lib.cz_tune(b"seglines", old)
         lib.cz_tune(b"pair", old_pair)
+
+
+def test_full_size_zipf_roundtrip(torch_dev, subkeys, L):
+    """BASELINE configs[3] at full size (2^20 Zipf frames, 64 B..64 KiB, 128-byte slots): segmented
+    seal -> segmented open is the identity with every status OK; sampled frames across the length
+    range equal the oracle; a tampered 64 KiB frame is rejected and its plaintext zeroed."""
+    torch, dev = torch_dev
+    from jeromq_amd import batch
+    rng = np.random.default_rng(42)
+    n = 1 << 20
+    j = np.empty(0, dtype=np.int64)
+    while len(j) < n:
+        z = rng.zipf(1.2, size=n)
+        j = np.concatenate([j, z[z <= 1024]])
+    lens = (64 * j[:n]).astype(np.uint64)
+    slot_in = lens
+    slot_out = (lens + np.uint64(33 + 127)) // np.uint64(128) * np.uint64(128)
+    desc = np.zeros(n, dtype=DESC_DTYPE)
+    desc["in_off"][1:] = np.cumsum(slot_in[:-1])
+    desc["out_off"][1:] = np.cumsum(slot_out[:-1])
+    desc["len"] = lens
+    desc["counter"] = 3 + np.arange(n, dtype=np.uint64)
+    desc["flags"] = (np.arange(n) % 8 == 0).astype(np.uint32)
+    desc["prev"] = -1
+    in_bytes, out_bytes = int(slot_in.sum()), int(slot_out.sum())
+    d_in = torch.empty(in_bytes, dtype=torch.uint8, device=dev)
+    batch.fill(d_in, 0x5EED0003)
+    d_out = torch.zeros(out_bytes, dtype=torch.uint8, device=dev)
+    d_desc = _dev(torch_dev, desc)
+    plan = batch.SegmentPlan(desc, open_=False).to(dev)
+    batch.seal_segments(d_desc, plan, d_in, d_out, subkeys[0:1])
+    # open: bodies in place, payloads into a fresh buffer laid out like the input
+    odesc = desc.copy()
+    odesc["in_off"], odesc["out_off"] = desc["out_off"], desc["in_off"]
+    odesc["len"] = lens + np.uint64(33)
+    odesc["counter"] = 2 + np.arange(n, dtype=np.uint64)        # floor = nonce - 1
+    odesc["flags"] = 0x100
+    big = int(np.argmax(lens))
+    d_out[int(desc["out_off"][big]) + 40000] ^= 1              # tamper inside a 64 KiB frame
+    d_odesc = _dev(torch_dev, odesc)
+    oplan = batch.SegmentPlan(odesc, open_=True).to(dev)
+    d_plain = torch.full((in_bytes,), 0x55, dtype=torch.uint8, device=dev)
+    status = torch.full((n,), -1, dtype=torch.int16, device=dev)
+    batch.open_segments(d_odesc, oplan, d_out, d_plain, subkeys[0:1], status)
+    torch.cuda.synchronize()
+    st = status.cpu().numpy().view(np.uint16)
+    assert st[big] & 0xff == L.CZ_STATUS_CRYPTO
+    ok = np.ones(n, dtype=bool)
+    ok[big] = False
+    assert not np.any(st[ok] & 0xff)
+    assert np.array_equal(st[ok] >> 8, desc["flags"][ok].astype(np.uint16))
+    b0, b1 = int(desc["in_off"][big]), int(desc["in_off"][big] + lens[big])
+    assert not d_plain[b0:b1].any()
+    assert torch.equal(d_plain[:b0], d_in[:b0]) and torch.equal(d_plain[b1:], d_in[b1:])
+    d_out[int(desc["out_off"][big]) + 40000] ^= 1
+    # sampled frames across the length range vs the oracle
+    order = np.argsort(lens, kind="stable")
+    picks = set(int(order[k]) for k in np.linspace(0, n - 1, 48).astype(int)) | {0, n - 1, big}
+    for i in sorted(picks):
+        io, oo, ln = int(desc["in_off"][i]), int(desc["out_off"][i]), int(lens[i])
+        p = d_in[io:io + ln].cpu().numpy().tobytes()
+        body = d_out[oo:oo + ln + 33].cpu().numpy().tobytes()
+        assert body == or_curve_encode(p, int(desc["flags"][i]), 3 + i, 0, PRECOM), f"frame {i} len {ln}"
+    del d_in, d_out, d_plain
+    torch.cuda.empty_cache()

@@ -9,7 +9,7 @@ import ctypes
 import os
 
 HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(HERE, "libcurvezmq_mi355x.so")
+LIB_PATH = os.environ.get("CZ_LIB", os.path.join(HERE, "libcurvezmq_mi355x.so"))  # CZ_LIB: A/B builds only
 
 CZ_OK = 0
 CZ_EINVAL = -22

@@ -52,6 +52,13 @@ enum Mode { MODE_ZMQ = 0, MODE_NACL = 1 };
 constexpr u32 HDR0 = 0x53454d07u, HDR1 = 0x45474153u;
 
 constexpr int BLOCK = 256;              // threads per workgroup (4 waves)
+// Build-time occupancy experiment knob (CZ_EXTRA_FLAGS=-DCZ_SEAL_WAVES_PER_EU=n): caps the VGPRs of
+// the uniform/segment kernels so that n waves fit per SIMD.
+#ifdef CZ_SEAL_WAVES_PER_EU
+#define CZ_OCC __attribute__((amdgpu_waves_per_eu(CZ_SEAL_WAVES_PER_EU, CZ_SEAL_WAVES_PER_EU)))
+#else
+#define CZ_OCC
+#endif
 constexpr int WAVES = BLOCK / 64;
 constexpr u32 LINE_LDS_BYTES = 64 * 128; // EmitLines: one 128-byte line per frame
 constexpr u32 REGION_MAX = 16384;       // EmitRegion: 64 slots per wave
@@ -1257,7 +1264,7 @@ enum Staging { ST_DIRECT = 0, ST_LINES = 1, ST_REGION = 2 };
 // ST_LINES / ST_REGION need the launcher's preconditions (see czk_seal_uniform);
 // a wave with fewer than 64 frames always stores directly.
 template <int ST, bool PAIR>
-__global__ __launch_bounds__(BLOCK) void k_seal_uniform(const uint8_t *__restrict__ in, uint64_t in_stride,
+__global__ __launch_bounds__(BLOCK) CZ_OCC void k_seal_uniform(const uint8_t *__restrict__ in, uint64_t in_stride,
                                                          uint8_t *__restrict__ out, uint64_t out_stride,
                                                          uint32_t count, uint32_t len,
                                                          const uint8_t *__restrict__ subkey, uint64_t counter0,
@@ -1374,7 +1381,7 @@ __global__ __launch_bounds__(BLOCK) void k_open_desc(const cz_frame_desc *__rest
 // Uniform open of one connection's bodies in order: frame i must beat frame
 // i-1's nonce, frame 0 must beat floor0 (when check != 0).
 template <int ST, bool PAIR>
-__global__ __launch_bounds__(BLOCK) void k_open_uniform(const uint8_t *__restrict__ in, uint64_t in_stride,
+__global__ __launch_bounds__(BLOCK) CZ_OCC void k_open_uniform(const uint8_t *__restrict__ in, uint64_t in_stride,
                                                          uint8_t *__restrict__ out, uint64_t out_stride,
                                                          uint32_t count, uint32_t size,
                                                          const uint8_t *__restrict__ subkey, uint64_t floor0,
@@ -1450,7 +1457,7 @@ __device__ __forceinline__ bool wave_lines_ok(bool full_wave, u32 nchunks, bool 
     return wave_uniform(nchunks) && __builtin_amdgcn_ballot_w64(!al) == 0;
 }
 
-__global__ __launch_bounds__(BLOCK) void k_seal_segments(const cz_frame_desc *__restrict__ desc,
+__global__ __launch_bounds__(BLOCK) CZ_OCC void k_seal_segments(const cz_frame_desc *__restrict__ desc,
                                                           const cz_segment *__restrict__ segs, uint32_t nseg,
                                                           const uint8_t *__restrict__ in, uint8_t *__restrict__ out,
                                                           const uint8_t *__restrict__ subkeys,

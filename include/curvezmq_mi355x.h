@@ -296,6 +296,11 @@ int cz_engine_flush_out(cz_engine *e);
 int cz_engine_wire_out(cz_engine *e, int conn, const uint8_t **wire, uint64_t *len);
 /* append bytes received on a connection (partial frames are kept for the next flush) */
 int cz_engine_recv(cz_engine *e, int conn, const void *wire, uint64_t len);
+/* zero-copy receive (the V2Decoder getBuffer() pattern, StreamEngine.java:403-410): a pinned
+ * buffer of *avail >= min_bytes bytes at the end of the connection's received data; read from
+ * the socket into it, then commit the bytes read.  Valid until the next engine call. */
+int cz_engine_recv_buffer(cz_engine *e, int conn, uint64_t min_bytes, uint8_t **buf, uint64_t *avail);
+int cz_engine_recv_commit(cz_engine *e, int conn, uint64_t n);
 /* parse, open and sequence-check every whole frame received on every connection */
 int cz_engine_flush_in(cz_engine *e);
 /* decoded messages of the last cz_engine_flush_in (pinned memory, valid until the next one) */

@@ -19,9 +19,12 @@
 //              bodies into aligned slots -> segmented open with the nonce floor chained frame to
 //              frame inside each connection (desc.prev) -> D2H -> per-connection delivery up to the
 //              first failing frame, whose status becomes the connection's error event.
+#include <stdio.h>
+#include <stdlib.h>
 #include <string.h>
 
 #include <algorithm>
+#include <chrono>
 #include <vector>
 
 #include "cz_internal.h"
@@ -35,6 +38,52 @@ constexpr uint32_t SEG_BLOCKS = 64;
 
 uint64_t round_up(uint64_t v, uint64_t a) { return (v + a - 1) / a * a; }
 
+// grow a pinned buffer to hold `want` bytes, keeping its first `used` bytes
+hipError_t grow_keep(HostBuf &b, uint64_t used, uint64_t want)
+{
+    if (want <= b.cap)
+        return hipSuccess;
+    void *p = nullptr;
+    const uint64_t cap = std::max<uint64_t>({want, 2 * b.cap, 65536});
+    hipError_t e = hipHostMalloc(&p, cap, hipHostMallocDefault);
+    if (e != hipSuccess)
+        return e;
+    if (used)
+        memcpy(p, b.ptr, used);
+    b.release();
+    b.ptr = p;
+    b.cap = cap;
+    return hipSuccess;
+}
+
+// CZ_ENGINE_TRACE=1: per-phase wall times of each flush on stderr (profiling aid)
+struct PhaseTimer {
+    bool on;
+    const char *what;
+    std::chrono::steady_clock::time_point t0, last;
+    char buf[512];
+    int len = 0;
+    explicit PhaseTimer(const char *w) : on(getenv("CZ_ENGINE_TRACE") != nullptr), what(w)
+    {
+        t0 = last = std::chrono::steady_clock::now();
+    }
+    void mark(const char *phase)
+    {
+        if (!on)
+            return;
+        auto now = std::chrono::steady_clock::now();
+        len += snprintf(buf + len, sizeof(buf) - len, " %s=%.2fms", phase,
+                        std::chrono::duration<double, std::milli>(now - last).count());
+        last = now;
+    }
+    ~PhaseTimer()
+    {
+        if (on)
+            fprintf(stderr, "[cz_engine] %s%s total=%.2fms\n", what, buf,
+                    std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count());
+    }
+};
+
 struct Conn {
     bool server = false;
     uint32_t tx_key = 0, rx_key = 0;  // subkey table indices
@@ -42,7 +91,8 @@ struct Conn {
     uint64_t peer_nonce = 0;          // cnPeerNonce: last accepted peer nonce
     int error = 0;                    // CZ_EPROTO / CZ_EMSGSIZE once torn down
     int event = 0;                    // ZMTP protocol-error event of the failure
-    std::vector<uint8_t> inbuf;       // received bytes not yet parsed (a partial frame)
+    HostBuf rx;                       // received bytes not yet parsed, pinned (DMA'd as they lie)
+    uint64_t rx_len = 0;
     uint64_t wire_off = 0, wire_len = 0;
     std::vector<uint32_t> in_msgs;    // indices into Engine::in_msgs of the last flush_in
 };
@@ -82,6 +132,10 @@ int plan(const std::vector<cz_frame_desc> &d, int open, Segs &s)
 struct cz_engine {
     int device = 0;
     hipStream_t stream = nullptr;
+    // flush_in pipeline: ps[0] carries every group's H2D in order; ps[1] waits for a group's
+    // copies (event), then runs its kernels and D2H -- so group g's D2H overlaps group g+1's H2D
+    static constexpr int PIPE = 3;
+    hipStream_t ps[PIPE] = {nullptr, nullptr, nullptr};
     std::vector<Conn> conns;
     DevBuf subkeys;  // 32 B per (connection, direction)
     uint32_t nkeys = 0;
@@ -92,11 +146,12 @@ struct cz_engine {
     HostBuf h_wire;
     uint64_t wire_total = 0;
     // inbound
-    HostBuf h_rx, h_plain;
+    HostBuf h_plain;
     std::vector<InMsg> in_msgs;
     // device staging (grows, never shrinks)
     DevBuf d_in, d_body, d_wire, d_desc, d_seg, d_comb, d_work, d_items, d_status, d_nonces, d_plain;
     HostBuf h_status, h_nonces;
+    HostBuf h_meta;  // pinned staging of descriptors / items / segment lists (async H2D)
 
     ~cz_engine()
     {
@@ -105,11 +160,18 @@ struct cz_engine {
             (void)hipStreamSynchronize(stream);
             (void)hipStreamDestroy(stream);
         }
+        for (hipStream_t &q : ps)
+            if (q) {
+                (void)hipStreamSynchronize(q);
+                (void)hipStreamDestroy(q);
+            }
         for (DevBuf *b : {&subkeys, &d_in, &d_body, &d_wire, &d_desc, &d_seg, &d_comb, &d_work, &d_items, &d_status,
                           &d_nonces, &d_plain})
             b->release();
-        for (HostBuf *b : {&arena, &h_wire, &h_rx, &h_plain, &h_status, &h_nonces})
+        for (HostBuf *b : {&arena, &h_wire, &h_plain, &h_status, &h_nonces, &h_meta})
             b->release();
+        for (Conn &c : conns)
+            c.rx.release();
     }
 
     Conn *conn(int c)
@@ -166,6 +228,7 @@ struct cz_engine {
 
     int flush_out()
     {
+        PhaseTimer pt("flush_out");
         for (Conn &c : conns)
             c.wire_off = c.wire_len = 0;
         wire_total = 0;
@@ -202,6 +265,7 @@ struct cz_engine {
             cursor[m.conn] += cz_v2_header_size(body) + body;
             slot += round_up(body, SLOT_ALIGN);
         }
+        pt.mark("desc");
         hipError_t e;
         if ((e = d_in.reserve(std::max<uint64_t>(arena_used, 16))) != hipSuccess ||
             (e = d_body.reserve(slot)) != hipSuccess || (e = d_wire.reserve(wire_total)) != hipSuccess ||
@@ -216,13 +280,19 @@ struct cz_engine {
         int rc = upload_and_plan(desc, 0, s);
         if (rc != CZ_OK)
             return rc;
+        pt.mark("h2d+plan");
         if ((e = czk_seal_segments((const cz_frame_desc *)d_desc.ptr, (const cz_segment *)d_seg.ptr, s.nseg,
                                    (const cz_combine *)d_comb.ptr, s.ncomb, d_in.ptr, d_body.ptr, subkeys.ptr,
                                    d_work.ptr, stream)) != hipSuccess ||
-            (e = czk_v2_copy((const cz_v2_item *)d_items.ptr, n, d_body.ptr, d_wire.ptr, stream)) != hipSuccess ||
-            (e = hipMemcpyAsync(h_wire.ptr, d_wire.ptr, wire_total, hipMemcpyDeviceToHost, stream)) != hipSuccess ||
+            (e = czk_v2_copy((const cz_v2_item *)d_items.ptr, n, d_body.ptr, d_wire.ptr, stream)) != hipSuccess)
+            return hip_fail(e, "cz_engine: flush_out");
+        if (pt.on && (e = hipStreamSynchronize(stream)) != hipSuccess)
+            return hip_fail(e, "cz_engine: flush_out");
+        pt.mark("kernels");
+        if ((e = hipMemcpyAsync(h_wire.ptr, d_wire.ptr, wire_total, hipMemcpyDeviceToHost, stream)) != hipSuccess ||
             (e = hipStreamSynchronize(stream)) != hipSuccess)
             return hip_fail(e, "cz_engine: flush_out");
+        pt.mark("d2h");
         pend.clear();
         arena_used = 0;
         return CZ_OK;
@@ -240,6 +310,7 @@ struct cz_engine {
 
     int flush_in()
     {
+        PhaseTimer pt("flush_in");
         in_msgs.clear();
         for (Conn &c : conns)
             c.in_msgs.clear();
@@ -247,7 +318,7 @@ struct cz_engine {
         struct Parsed {
             uint32_t conn;
             uint32_t first, count;  // range in frames
-            uint64_t rx_off;        // where the connection's whole-frame bytes start in h_rx
+            uint64_t rx_off;        // where the connection's whole-frame bytes start in d_wire
             uint64_t consumed;
             int perr;               // framing error after the parsed frames
         };
@@ -256,10 +327,10 @@ struct cz_engine {
         uint64_t rx_total = 0;
         for (size_t ci = 0; ci < conns.size(); ci++) {
             Conn &c = conns[ci];
-            if (c.error || c.inbuf.empty())
+            if (c.error || c.rx_len == 0)
                 continue;
             // parse in chunks of CH frames (a frame is >= 2 bytes, so sizing by bytes would cost 8x the data)
-            constexpr uint32_t CH = 65536;
+            constexpr uint32_t CH = 4096;
             const size_t base = frames.size();
             uint64_t consumed = 0;
             int prc = CZ_OK;
@@ -268,8 +339,8 @@ struct cz_engine {
                 frames.resize(at + CH);
                 uint32_t nf = 0;
                 uint64_t used = 0;
-                prc = cz_v2_parse(c.inbuf.data() + consumed, c.inbuf.size() - consumed, -1, frames.data() + at, CH,
-                                  &nf, &used);
+                prc = cz_v2_parse((const uint8_t *)c.rx.ptr + consumed, c.rx_len - consumed, -1, frames.data() + at,
+                                  CH, &nf, &used);
                 frames.resize(at + nf);
                 for (uint32_t k = 0; k < nf; k++)
                     frames[at + k].body_off += consumed;
@@ -283,26 +354,50 @@ struct cz_engine {
         }
         const uint32_t n = (uint32_t)frames.size();
         hipError_t e;
-        if ((e = h_rx.reserve(std::max<uint64_t>(rx_total, 16))) != hipSuccess)
-            return hip_fail(e, "cz_engine: alloc");
-        for (const Parsed &p : parsed)
-            memcpy((uint8_t *)h_rx.ptr + p.rx_off, conns[p.conn].inbuf.data(), p.consumed);
-        // 2. descriptors: bodies unpacked into aligned slots, each connection's frames chained by prev
+        pt.mark("parse");
+        // 2. connection groups of ~equal bytes (pipelined below), then descriptors: bodies unpacked
+        //    into aligned slots, each connection's frames chained by prev (group-relative indices)
+        struct Group {
+            size_t pa, pb;        // parsed[pa, pb)
+            uint32_t fa, fb;      // frames[fa, fb)
+            uint64_t pl0, pl1;    // plaintext slot range
+        };
+        std::vector<Group> groups;
+        {
+            const int G = rx_total >= (64ull << 20) ? 8 : 1;
+            size_t pa = 0;
+            uint64_t acc = 0;
+            for (size_t q = 0; q < parsed.size(); q++) {
+                acc += parsed[q].consumed;
+                const bool last = q + 1 == parsed.size();
+                if (last || acc * G >= rx_total * (groups.size() + 1)) {
+                    groups.push_back({pa, q + 1, 0, 0, 0, 0});
+                    pa = q + 1;
+                }
+            }
+        }
         std::vector<cz_frame_desc> desc(n);
         std::vector<cz_v2_item> items(n);
         uint64_t bslot = 0, pslot = 0;
-        for (const Parsed &p : parsed) {
-            const Conn &c = conns[p.conn];
-            for (uint32_t k = 0; k < p.count; k++) {
-                const uint32_t i = p.first + k;
-                const cz_v2_frame &f = frames[i];
-                const uint64_t plen = f.size > CZ_MESSAGE_OVERHEAD ? f.size - CZ_MESSAGE_OVERHEAD : 0;
-                items[i] = {p.rx_off + f.body_off, bslot, f.size, 0u};
-                desc[i] = {bslot, pslot, f.size, c.rx_key, c.peer_nonce, CZ_DESC_CHECK_NONCE,
-                           k ? (int32_t)(i - 1) : -1};
-                bslot += round_up(std::max<uint64_t>(f.size, 1), SLOT_ALIGN);
-                pslot += round_up(std::max<uint64_t>(plen, 1), SLOT_ALIGN);
+        for (Group &g : groups) {
+            g.fa = g.pa < parsed.size() ? parsed[g.pa].first : n;
+            g.pl0 = pslot;
+            for (size_t q = g.pa; q < g.pb; q++) {
+                const Parsed &p = parsed[q];
+                const Conn &c = conns[p.conn];
+                for (uint32_t k = 0; k < p.count; k++) {
+                    const uint32_t i = p.first + k;
+                    const cz_v2_frame &f = frames[i];
+                    const uint64_t plen = f.size > CZ_MESSAGE_OVERHEAD ? f.size - CZ_MESSAGE_OVERHEAD : 0;
+                    items[i] = {p.rx_off + f.body_off, bslot, f.size, 0u};
+                    desc[i] = {bslot, pslot, f.size, c.rx_key, c.peer_nonce, CZ_DESC_CHECK_NONCE,
+                               k ? (int32_t)(i - 1 - g.fa) : -1};
+                    bslot += round_up(std::max<uint64_t>(f.size, 1), SLOT_ALIGN);
+                    pslot += round_up(std::max<uint64_t>(plen, 1), SLOT_ALIGN);
+                }
             }
+            g.fb = g.pb > g.pa ? parsed[g.pb - 1].first + parsed[g.pb - 1].count : g.fa;
+            g.pl1 = pslot;
         }
         if (n) {
             if ((e = d_wire.reserve(rx_total)) != hipSuccess || (e = d_in.reserve(bslot)) != hipSuccess ||
@@ -313,27 +408,108 @@ struct cz_engine {
                 (e = h_plain.reserve(pslot)) != hipSuccess || (e = h_status.reserve((uint64_t)n * 2)) != hipSuccess ||
                 (e = h_nonces.reserve((uint64_t)n * 8)) != hipSuccess)
                 return hip_fail(e, "cz_engine: alloc");
-            if ((e = hipMemcpyAsync(d_wire.ptr, h_rx.ptr, rx_total, hipMemcpyHostToDevice, stream)) != hipSuccess ||
-                (e = hipMemcpyAsync(d_items.ptr, items.data(), (uint64_t)n * sizeof(cz_v2_item),
-                                    hipMemcpyHostToDevice, stream)) != hipSuccess)
-                return hip_fail(e, "cz_engine: H2D");
-            Segs s;
-            int rc = upload_and_plan(desc, 1, s);
-            if (rc != CZ_OK)
-                return rc;
-            if ((e = czk_v2_copy((const cz_v2_item *)d_items.ptr, n, d_wire.ptr, d_in.ptr, stream)) != hipSuccess ||
-                (e = czk_open_segments((const cz_frame_desc *)d_desc.ptr, (const cz_segment *)d_seg.ptr, s.nseg,
-                                       (const cz_combine *)d_comb.ptr, s.ncomb, d_in.ptr, d_plain.ptr, subkeys.ptr,
-                                       d_work.ptr, (uint16_t *)d_status.ptr, (uint64_t *)d_nonces.ptr, stream)) !=
-                    hipSuccess ||
-                (e = hipMemcpyAsync(h_plain.ptr, d_plain.ptr, pslot, hipMemcpyDeviceToHost, stream)) != hipSuccess ||
-                (e = hipMemcpyAsync(h_status.ptr, d_status.ptr, (uint64_t)n * 2, hipMemcpyDeviceToHost, stream)) !=
-                    hipSuccess ||
-                (e = hipMemcpyAsync(h_nonces.ptr, d_nonces.ptr, (uint64_t)n * 8, hipMemcpyDeviceToHost, stream)) !=
-                    hipSuccess ||
-                (e = hipStreamSynchronize(stream)) != hipSuccess)
-                return hip_fail(e, "cz_engine: flush_in");
+            // plans per group; device segment / combine / work arrays hold all groups at once
+            std::vector<Segs> gs(groups.size());
+            uint64_t nseg = 0, ncomb = 0, npart = 0;
+            std::vector<uint64_t> soff(groups.size()), coff(groups.size()), woff(groups.size());
+            for (size_t gi = 0; gi < groups.size(); gi++) {
+                const Group &g = groups[gi];
+                std::vector<cz_frame_desc> sub(desc.begin() + g.fa, desc.begin() + g.fb);
+                int rc = plan(sub, 1, gs[gi]);
+                if (rc != CZ_OK)
+                    return rc;
+                soff[gi] = nseg;
+                coff[gi] = ncomb;
+                woff[gi] = npart;
+                nseg += gs[gi].nseg;
+                ncomb += gs[gi].ncomb;
+                npart += gs[gi].npart;
+            }
+            // pinned copies of the host-built arrays: pageable sources would make each H2D synchronous
+            const uint64_t m_items = 0, m_desc = (uint64_t)n * sizeof(cz_v2_item),
+                           m_seg = m_desc + (uint64_t)n * sizeof(cz_frame_desc),
+                           m_comb = m_seg + nseg * sizeof(cz_segment), m_end = m_comb + ncomb * sizeof(cz_combine);
+            if ((e = d_desc.reserve((uint64_t)n * sizeof(cz_frame_desc))) != hipSuccess ||
+                (e = d_seg.reserve(std::max<uint64_t>(nseg, 1) * sizeof(cz_segment))) != hipSuccess ||
+                (e = d_comb.reserve(std::max<uint64_t>(ncomb, 1) * sizeof(cz_combine))) != hipSuccess ||
+                (e = d_work.reserve(std::max<uint64_t>(npart, 1) * 64)) != hipSuccess ||
+                (e = h_meta.reserve(m_end)) != hipSuccess)
+                return hip_fail(e, "cz_engine: alloc");
+            uint8_t *hm = (uint8_t *)h_meta.ptr;
+            memcpy(hm + m_items, items.data(), (uint64_t)n * sizeof(cz_v2_item));
+            memcpy(hm + m_desc, desc.data(), (uint64_t)n * sizeof(cz_frame_desc));
+            for (size_t gi = 0; gi < groups.size(); gi++) {
+                memcpy(hm + m_seg + soff[gi] * sizeof(cz_segment), gs[gi].seg.data(),
+                       (uint64_t)gs[gi].nseg * sizeof(cz_segment));
+                memcpy(hm + m_comb + coff[gi] * sizeof(cz_combine), gs[gi].comb.data(),
+                       (uint64_t)gs[gi].ncomb * sizeof(cz_combine));
+            }
+            const cz_v2_item *h_items = (const cz_v2_item *)(hm + m_items);
+            const cz_frame_desc *h_desc = (const cz_frame_desc *)(hm + m_desc);
+            const cz_segment *h_seg = (const cz_segment *)(hm + m_seg);
+            const cz_combine *h_comb = (const cz_combine *)(hm + m_comb);
+            pt.mark("desc+plan");
+            std::vector<hipEvent_t> ev(groups.size(), nullptr);
+            for (hipEvent_t &x : ev)
+                if ((e = hipEventCreateWithFlags(&x, hipEventDisableTiming)) != hipSuccess)
+                    return hip_fail(e, "hipEventCreate");
+            struct EvGuard {
+                std::vector<hipEvent_t> &v;
+                ~EvGuard()
+                {
+                    for (hipEvent_t x : v)
+                        if (x)
+                            (void)hipEventDestroy(x);
+                }
+            } evguard{ev};
+            hipStream_t qh = ps[0], qk = ps[1];
+            for (size_t gi = 0; gi < groups.size(); gi++) {
+                const Group &g = groups[gi];
+                const uint32_t gn = g.fb - g.fa;
+                // (a) copy stream: the group's received bytes (straight from each connection's pinned
+                //     buffer) and its descriptors / items / segment lists
+                for (size_t pi = g.pa; pi < g.pb; pi++) {
+                    const Parsed &p = parsed[pi];
+                    if (p.consumed && (e = hipMemcpyAsync((uint8_t *)d_wire.ptr + p.rx_off, conns[p.conn].rx.ptr,
+                                                          p.consumed, hipMemcpyHostToDevice, qh)) != hipSuccess)
+                        return hip_fail(e, "cz_engine: H2D");
+                }
+                if (gn == 0)
+                    continue;
+                const Segs &sg = gs[gi];
+                cz_frame_desc *dd = (cz_frame_desc *)d_desc.ptr + g.fa;
+                cz_segment *dsg = (cz_segment *)d_seg.ptr + soff[gi];
+                cz_combine *dcb = (cz_combine *)d_comb.ptr + coff[gi];
+                if ((e = hipMemcpyAsync((cz_v2_item *)d_items.ptr + g.fa, h_items + g.fa,
+                                        (uint64_t)gn * sizeof(cz_v2_item), hipMemcpyHostToDevice, qh)) != hipSuccess ||
+                    (e = hipMemcpyAsync(dd, h_desc + g.fa, (uint64_t)gn * sizeof(cz_frame_desc),
+                                        hipMemcpyHostToDevice, qh)) != hipSuccess ||
+                    (sg.nseg && (e = hipMemcpyAsync(dsg, h_seg + soff[gi], (uint64_t)sg.nseg * sizeof(cz_segment),
+                                                    hipMemcpyHostToDevice, qh)) != hipSuccess) ||
+                    (sg.ncomb && (e = hipMemcpyAsync(dcb, h_comb + coff[gi], (uint64_t)sg.ncomb * sizeof(cz_combine),
+                                                     hipMemcpyHostToDevice, qh)) != hipSuccess) ||
+                    (e = hipEventRecord(ev[gi], qh)) != hipSuccess)
+                    return hip_fail(e, "cz_engine: flush_in H2D");
+                // (b) compute stream: once the group's copies landed, unpack + open, then D2H
+                if ((e = hipStreamWaitEvent(qk, ev[gi], 0)) != hipSuccess ||
+                    (e = czk_v2_copy((const cz_v2_item *)d_items.ptr + g.fa, gn, d_wire.ptr, d_in.ptr, qk)) !=
+                        hipSuccess ||
+                    (e = czk_open_segments(dd, dsg, sg.nseg, dcb, sg.ncomb, d_in.ptr, d_plain.ptr, subkeys.ptr,
+                                           (uint8_t *)d_work.ptr + 64 * woff[gi], (uint16_t *)d_status.ptr + g.fa,
+                                           (uint64_t *)d_nonces.ptr + g.fa, qk)) != hipSuccess ||
+                    (e = hipMemcpyAsync((uint8_t *)h_plain.ptr + g.pl0, (uint8_t *)d_plain.ptr + g.pl0,
+                                        g.pl1 - g.pl0, hipMemcpyDeviceToHost, qk)) != hipSuccess ||
+                    (e = hipMemcpyAsync((uint16_t *)h_status.ptr + g.fa, (uint16_t *)d_status.ptr + g.fa,
+                                        (uint64_t)gn * 2, hipMemcpyDeviceToHost, qk)) != hipSuccess ||
+                    (e = hipMemcpyAsync((uint64_t *)h_nonces.ptr + g.fa, (uint64_t *)d_nonces.ptr + g.fa,
+                                        (uint64_t)gn * 8, hipMemcpyDeviceToHost, qk)) != hipSuccess)
+                    return hip_fail(e, "cz_engine: flush_in");
+            }
+            for (hipStream_t q : ps)
+                if ((e = hipStreamSynchronize(q)) != hipSuccess)
+                    return hip_fail(e, "cz_engine: flush_in");
         }
+        pt.mark("h2d+kernels+d2h");
         // 3. deliver in order per connection, up to the first failure (decodeAndPush returns false)
         const uint16_t *st = (const uint16_t *)h_status.ptr;
         const uint64_t *nn = (const uint64_t *)h_nonces.ptr;
@@ -360,16 +536,21 @@ struct cz_engine {
                 in_msgs.push_back({desc[i].out_off, desc[i].len - CZ_MESSAGE_OVERHEAD, mf});
             }
             if (failed) {
-                c.inbuf.clear();
+                c.rx_len = 0;
                 continue;
             }
-            c.inbuf.erase(c.inbuf.begin(), c.inbuf.begin() + (ptrdiff_t)p.consumed);
+            // keep the partial frame for the next read
+            if (p.consumed) {
+                memmove(c.rx.ptr, (uint8_t *)c.rx.ptr + p.consumed, c.rx_len - p.consumed);
+                c.rx_len -= p.consumed;
+            }
             if (p.perr) {  // V2Decoder error after the good frames: StreamEngine error(PROTOCOL)
                 c.error = p.perr;
                 c.event = 0;
-                c.inbuf.clear();
+                c.rx_len = 0;
             }
         }
+        pt.mark("deliver");
         return CZ_OK;
     }
 };
@@ -389,6 +570,9 @@ int cz_engine_create(cz_engine **out, uint64_t arena_bytes, int device)
     hipError_t he;
     if ((he = hipSetDevice(device)) != hipSuccess ||
         (he = hipStreamCreateWithFlags(&e->stream, hipStreamNonBlocking)) != hipSuccess ||
+        (he = hipStreamCreateWithFlags(&e->ps[0], hipStreamNonBlocking)) != hipSuccess ||
+        (he = hipStreamCreateWithFlags(&e->ps[1], hipStreamNonBlocking)) != hipSuccess ||
+        (he = hipStreamCreateWithFlags(&e->ps[2], hipStreamNonBlocking)) != hipSuccess ||
         (he = e->arena.reserve(std::max<uint64_t>(arena_bytes, 4096))) != hipSuccess) {
         delete e;
         return hip_fail(he, "cz_engine_create");
@@ -507,8 +691,42 @@ int cz_engine_recv(cz_engine *e, int conn, const void *wire, uint64_t len)
         return CZ_EINVAL;
     if (c->error)
         return fail(c->error, "cz_engine_recv: connection %d has failed", conn);
-    const uint8_t *p = (const uint8_t *)wire;
-    c->inbuf.insert(c->inbuf.end(), p, p + len);
+    hipError_t he = grow_keep(c->rx, c->rx_len, c->rx_len + len);
+    if (he != hipSuccess)
+        return hip_fail(he, "cz_engine_recv: hipHostMalloc");
+    if (len)
+        memcpy((uint8_t *)c->rx.ptr + c->rx_len, wire, len);
+    c->rx_len += len;
+    return CZ_OK;
+}
+
+int cz_engine_recv_buffer(cz_engine *e, int conn, uint64_t min_bytes, uint8_t **buf, uint64_t *avail)
+{
+    if (!e || !buf || !avail)
+        return fail(CZ_EINVAL, "cz_engine_recv_buffer: null pointer");
+    Conn *c = e->conn(conn);
+    if (!c)
+        return CZ_EINVAL;
+    if (c->error)
+        return fail(c->error, "cz_engine_recv_buffer: connection %d has failed", conn);
+    hipError_t he = grow_keep(c->rx, c->rx_len, c->rx_len + std::max<uint64_t>(min_bytes, 1));
+    if (he != hipSuccess)
+        return hip_fail(he, "cz_engine_recv_buffer: hipHostMalloc");
+    *buf = (uint8_t *)c->rx.ptr + c->rx_len;
+    *avail = c->rx.cap - c->rx_len;
+    return CZ_OK;
+}
+
+int cz_engine_recv_commit(cz_engine *e, int conn, uint64_t n)
+{
+    if (!e)
+        return fail(CZ_EINVAL, "cz_engine_recv_commit: null engine");
+    Conn *c = e->conn(conn);
+    if (!c)
+        return CZ_EINVAL;
+    if (n > c->rx.cap - c->rx_len)
+        return fail(CZ_EINVAL, "cz_engine_recv_commit: %llu bytes exceed the buffer", (unsigned long long)n);
+    c->rx_len += n;
     return CZ_OK;
 }
 

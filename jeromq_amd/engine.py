@@ -74,6 +74,17 @@ class CurveBatchEngine:
         buf = ctypes.create_string_buffer(b, len(b)) if b else None
         return self._L.cz_engine_recv(self._h, conn, buf, len(b))
 
+    def recv_into(self, conn, read, max_bytes=1 << 20):
+        """Zero-copy receive: `read(memoryview)` fills the engine's pinned buffer (e.g.
+        sock.recv_into) and returns the byte count, which is committed."""
+        p, n = ctypes.c_void_p(), ctypes.c_uint64()
+        _lib.check(self._L.cz_engine_recv_buffer(self._h, conn, max_bytes, ctypes.byref(p), ctypes.byref(n)),
+                   "cz_engine_recv_buffer")
+        view = memoryview((ctypes.c_uint8 * n.value).from_address(p.value)).cast("B")
+        got = read(view)
+        _lib.check(self._L.cz_engine_recv_commit(self._h, conn, got), "cz_engine_recv_commit")
+        return got
+
     def flush_in(self):
         _lib.check(self._L.cz_engine_flush_in(self._h), "cz_engine_flush_in")
 

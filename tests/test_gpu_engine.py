@@ -180,3 +180,34 @@ def test_engine_failures_tear_down_one_connection(torch_dev, L):
     # a torn-down connection refuses further traffic; the others keep working
     assert srv.recv(sc[1], b"\x00\x01x") == L.CZ_EPROTO
     assert srv.send(sc[0], b"still fine") == 0
+
+
+def test_engine_zero_copy_receive_from_socket(torch_dev, L):
+    """cz_engine_recv_buffer / _commit: bytes read from a socket straight into the engine's
+    pinned buffer (the V2Decoder getBuffer() pattern), in small reads that split frames."""
+    import socket
+    from jeromq_amd.engine import CurveBatchEngine
+    cli = CurveBatchEngine(arena_bytes=1 << 20)
+    srv = CurveBatchEngine(arena_bytes=1 << 20)
+    c = cli.add_connection(PRECOM)
+    s = srv.add_connection(PRECOM, as_server=True)
+    msgs = [(splitmix_bytes(n, 60 + n), n % 2) for n in (0, 17, 255, 256, 3000, 40000)]
+    for p, fl in msgs:
+        cli.send(c, p, more=bool(fl))
+    cli.flush_out()
+    w = cli.wire_out(c)
+    a, b = socket.socketpair()
+    try:
+        a.sendall(w)
+        a.shutdown(socket.SHUT_WR)
+        got = []
+        while True:
+            n = srv.recv_into(s, lambda mv: b.recv_into(mv, 777), max_bytes=777)
+            if n == 0:
+                break
+            srv.flush_in()
+            got += srv.messages_in(s)
+    finally:
+        a.close()
+        b.close()
+    assert srv.error(s) == (0, 0) and got == msgs

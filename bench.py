@@ -43,6 +43,8 @@ def parse():
                     help="untimed launches before the W warmup steps until this much GPU time has passed: "
                          "the clock needs ~100 ms of load to leave its idle state")
     ap.add_argument("--seg-blocks", type=int, default=64, help="zipf: segment length in 64-byte blocks")
+    ap.add_argument("--in-align", type=int, default=64,
+                    help="zipf: input payload slot alignment in bytes (lengths are 64-byte multiples)")
     ap.add_argument("--out-align", type=int, default=128,
                     help="zipf: output slot alignment in bytes (the caller's packing choice)")
     ap.add_argument("--config", default="4k", choices=["4k", "100b", "zipf", "zipf_lane", "open4k", "e2e4k", "engine", "beforenm"])
@@ -113,7 +115,7 @@ def shard_plan(rank, frames_per_rank, cfg="4k"):
 class Workload:
     """Builds one rank's device-resident batch and the per-step launch."""
 
-    def __init__(self, cfg, frames, rank, dev, out_align=128, seg_blocks=64):
+    def __init__(self, cfg, frames, rank, dev, out_align=128, seg_blocks=64, in_align=64):
         self.cfg = cfg
         self.dev = dev
         key = torch.tensor(list(PRECOM), dtype=torch.uint8, device=dev).view(1, 32)
@@ -152,8 +154,10 @@ class Workload:
                 j = np.concatenate([j, z[z <= 1024]])
             lens = (64 * j[:frames]).astype(np.uint64)
             desc = np.zeros(frames, dtype=batch.DESC_DTYPE)
+            ia = np.uint64(in_align)
+            in_len = (lens + ia - np.uint64(1)) // ia * ia
             in_off = np.zeros(frames, dtype=np.uint64)
-            in_off[1:] = np.cumsum(lens[:-1])
+            in_off[1:] = np.cumsum(in_len[:-1])
             al = np.uint64(out_align)
             out_len = (lens + np.uint64(33) + al - np.uint64(1)) // al * al
             out_off = np.zeros(frames, dtype=np.uint64)
@@ -165,21 +169,22 @@ class Workload:
             desc["flags"] = (np.arange(frames) % 8 == 0).astype(np.uint32)
             desc["prev"] = -1
             self.desc_np = desc
-            in_bytes = int(lens.sum())
+            in_bytes = int(in_len.sum())
             out_bytes = int(out_len.sum())
             self.d_in = torch.empty(in_bytes, dtype=torch.uint8, device=dev)
             batch.fill(self.d_in, seed)
             self.d_out = torch.empty(out_bytes, dtype=torch.uint8, device=dev)
             self.d_desc = torch.from_numpy(desc.view(np.uint8)).to(dev)
-            self.payload_bytes = in_bytes
+            pay = int(lens.sum())
+            self.payload_bytes = pay
             if cfg == "zipf":
                 # long frames split into 64-block segments (one lane each) + Poly1305 combine
                 self.plan = batch.SegmentPlan(desc, open_=False, seg_blocks=seg_blocks).to(dev)
-                self.read_bytes = in_bytes + 40 * frames + 16 * self.plan.nseg + 16 * self.plan.ncomb
+                self.read_bytes = pay + 40 * frames + 16 * self.plan.nseg + 16 * self.plan.ncomb
             else:  # zipf_lane: one lane per frame, longest first
                 order = batch.plan_order(desc)
                 self.d_order = torch.from_numpy(order.view(np.int32)).to(dev)
-                self.read_bytes = in_bytes + 40 * frames + 4 * frames
+                self.read_bytes = pay + 40 * frames + 4 * frames
             self.write_bytes = int((lens + np.uint64(33)).sum())
             self.n = None
         torch.cuda.synchronize()
@@ -485,7 +490,8 @@ def main():
         if rank == 0:
             print(json.dumps(line), flush=True)
         return
-    wl = Workload(args.config, args.frames, rank, dev, out_align=args.out_align, seg_blocks=args.seg_blocks)
+    wl = Workload(args.config, args.frames, rank, dev, out_align=args.out_align, seg_blocks=args.seg_blocks,
+                  in_align=args.in_align)
 
     ramp = 0
     t_ramp = time.perf_counter()

@@ -10,6 +10,8 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+#include "cz_salsa_lazy.h"
+
 namespace cz {
 
 typedef uint32_t u32;
@@ -28,47 +30,92 @@ __device__ __forceinline__ void qr(u32 &a, u32 &b, u32 &c, u32 &d)
     a ^= rotl(d + c, 18);
 }
 
-__device__ __forceinline__ void double_rounds(u32 x[16])
+__device__ __forceinline__ void col_round(u32 x[16])
 {
+    qr(x[0], x[4], x[8], x[12]);
+    qr(x[5], x[9], x[13], x[1]);
+    qr(x[10], x[14], x[2], x[6]);
+    qr(x[15], x[3], x[7], x[11]);
+}
+
+__device__ __forceinline__ void row_round(u32 x[16])
+{
+    qr(x[0], x[1], x[2], x[3]);
+    qr(x[5], x[6], x[7], x[4]);
+    qr(x[10], x[11], x[8], x[9]);
+    qr(x[15], x[12], x[13], x[14]);
+}
+
+// The 20 Salsa20 rounds with LAZY XORS (cz_salsa_lazy.h, generated and self-checked by
+// tools/gen_salsa_lazy.py).  Every int32 VALU instruction costs its SIMD 4 cycles on gfx950
+// whatever the opcode (tools/diag/salsa_ub.hip), so a block costs its instruction count.
+// Round 1 stays in C: its 3 wave-uniform quarter-rounds (constants, key, block counter, high
+// nonce word) go to the scalar unit.  Rounds 2..20 keep most `w ^= R` updates pending and let
+// v_xad_u32 ((a ^ b) + c) and v_bitop3_b32 (a ^ b ^ c) absorb them: 776 VALU instead of 912.
+// On return word w is x[w] ^ d[w] for the bits of CZ_LAZY_PENDING, x[w] otherwise.
+// -DCZ_SALSA_EAGER builds the plain rounds (A/B experiments).
+__device__ __forceinline__ void rounds_lazy(u32 x[16], u32 d[16])
+{
+    col_round(x);
+#ifdef CZ_SALSA_EAGER
+    row_round(x);
 #pragma unroll
-    for (int i = 0; i < 10; i++) {
-        qr(x[0], x[4], x[8], x[12]);
-        qr(x[5], x[9], x[13], x[1]);
-        qr(x[10], x[14], x[2], x[6]);
-        qr(x[15], x[3], x[7], x[11]);
-        qr(x[0], x[1], x[2], x[3]);
-        qr(x[5], x[6], x[7], x[4]);
-        qr(x[10], x[11], x[8], x[9]);
-        qr(x[15], x[12], x[13], x[14]);
+    for (int i = 1; i < 10; i++) {
+        col_round(x);
+        row_round(x);
     }
+#pragma unroll
+    for (int k = 0; k < 16; k++)
+        d[k] = 0u;
+#else
+    u32 t0, t1, t2, t3;
+    asm(CZ_SALSA_R2_20_ASM
+        : "+v"(x[0]), "+v"(x[1]), "+v"(x[2]), "+v"(x[3]), "+v"(x[4]), "+v"(x[5]), "+v"(x[6]), "+v"(x[7]),
+          "+v"(x[8]), "+v"(x[9]), "+v"(x[10]), "+v"(x[11]), "+v"(x[12]), "+v"(x[13]), "+v"(x[14]), "+v"(x[15]),
+          "=&v"(d[0]), "=&v"(d[1]), "=&v"(d[2]), "=&v"(d[3]), "=&v"(d[4]), "=&v"(d[5]), "=&v"(d[6]), "=&v"(d[7]),
+          "=&v"(d[8]), "=&v"(d[9]), "=&v"(d[10]), "=&v"(d[11]), "=&v"(d[12]), "=&v"(d[13]), "=&v"(d[14]),
+          "=&v"(d[15]), "=&v"(t0), "=&v"(t1), "=&v"(t2), "=&v"(t3));
+#endif
+}
+
+__device__ __forceinline__ constexpr bool lazy_pending(int k)
+{
+#ifdef CZ_SALSA_EAGER
+    return k < 0;
+#else
+    return (CZ_LAZY_PENDING >> k) & 1u;
+#endif
 }
 
 // One Salsa20/20 block: key k[8] (LE words), nonce words n0,n1 (LE loads of
 // nonce bytes 16..23 of the XSalsa20 nonce), 64-bit block counter c0|c1.
+// The feed-forward add absorbs the deltas rounds_lazy left pending (v_xad_u32).
 __device__ __forceinline__ void salsa20_block(u32 x[16], const u32 k[8], u32 n0, u32 n1, u32 c0, u32 c1)
 {
-    x[0] = SIGMA0; x[1] = k[0]; x[2] = k[1]; x[3] = k[2];
-    x[4] = k[3]; x[5] = SIGMA1; x[6] = n0; x[7] = n1;
-    x[8] = c0; x[9] = c1; x[10] = SIGMA2; x[11] = k[4];
-    x[12] = k[5]; x[13] = k[6]; x[14] = k[7]; x[15] = SIGMA3;
-    double_rounds(x);
-    x[0] += SIGMA0; x[1] += k[0]; x[2] += k[1]; x[3] += k[2];
-    x[4] += k[3]; x[5] += SIGMA1; x[6] += n0; x[7] += n1;
-    x[8] += c0; x[9] += c1; x[10] += SIGMA2; x[11] += k[4];
-    x[12] += k[5]; x[13] += k[6]; x[14] += k[7]; x[15] += SIGMA3;
+    const u32 in[16] = {SIGMA0, k[0], k[1], k[2], k[3], SIGMA1, n0, n1, c0, c1, SIGMA2, k[4], k[5], k[6], k[7], SIGMA3};
+    u32 d[16];
+#pragma unroll
+    for (int i = 0; i < 16; i++)
+        x[i] = in[i];
+    rounds_lazy(x, d);
+#pragma unroll
+    for (int i = 0; i < 16; i++)
+        x[i] = lazy_pending(i) ? ((x[i] ^ d[i]) + in[i]) : (x[i] + in[i]);
 }
 
 // HSalsa20(k, in16) -> out[8]: no feed-forward, words 0,5,10,15,6,7,8,9.
 __device__ __forceinline__ void hsalsa20(u32 out[8], const u32 k[8], const u32 in[4])
 {
-    u32 x[16];
+    u32 x[16], d[16];
     x[0] = SIGMA0; x[1] = k[0]; x[2] = k[1]; x[3] = k[2];
     x[4] = k[3]; x[5] = SIGMA1; x[6] = in[0]; x[7] = in[1];
     x[8] = in[2]; x[9] = in[3]; x[10] = SIGMA2; x[11] = k[4];
     x[12] = k[5]; x[13] = k[6]; x[14] = k[7]; x[15] = SIGMA3;
-    double_rounds(x);
-    out[0] = x[0]; out[1] = x[5]; out[2] = x[10]; out[3] = x[15];
-    out[4] = x[6]; out[5] = x[7]; out[6] = x[8]; out[7] = x[9];
+    rounds_lazy(x, d);
+    constexpr int w[8] = {0, 5, 10, 15, 6, 7, 8, 9};
+#pragma unroll
+    for (int i = 0; i < 8; i++)
+        out[i] = lazy_pending(w[i]) ? (x[w[i]] ^ d[w[i]]) : x[w[i]];
 }
 
 // ---- Poly1305, radix 2^32 ------------------------------------------------

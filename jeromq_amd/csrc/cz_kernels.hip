@@ -170,6 +170,15 @@ struct EmitDirect {
             }
         }
     }
+    // chunk q lies entirely inside the object (64q + 64 <= total): no tail handling
+    __device__ __forceinline__ void emit_full(u32 q, const u32 D[16])
+    {
+        uint8_t *p = dst + 64u * q;
+        st16<AL>(p, D[0], D[1], D[2], D[3]);
+        st16<AL>(p + 16, D[4], D[5], D[6], D[7]);
+        st16<AL>(p + 32, D[8], D[9], D[10], D[11]);
+        st16<AL>(p + 48, D[12], D[13], D[14], D[15]);
+    }
     __device__ __forceinline__ void tag(const u32 t[4]) { st16<AL>(dst + 16, t[0], t[1], t[2], t[3]); }
     __device__ __forceinline__ void finish() {}
     __device__ __forceinline__ void close(bool bad)
@@ -226,6 +235,12 @@ struct EmitLines {
             D[k] = Din[k];
         if (64u * q + 64u > total)
             mask_chunk(D, total > 64u * q ? total - 64u * q : 0u);
+        emit_full(q, D);
+    }
+    // chunk q lies entirely inside the object: no masking, so no branch (and no register
+    // copies merging masked and unmasked chunks) between the producer and the LDS writes
+    __device__ __forceinline__ void emit_full(u32 q, const u32 D[16])
+    {
         const u32 h = q & 1u;
         const u32 sw = lane & 7u;
 #pragma unroll
@@ -288,6 +303,13 @@ struct EmitRegion {
         for (u32 c = 0; c < 4; c++)
             if (64u * q + 16u * c < stride)
                 lds[base + c] = make_uint4(D[4 * c], D[4 * c + 1], D[4 * c + 2], D[4 * c + 3]);
+    }
+    __device__ __forceinline__ void emit_full(u32 q, const u32 D[16])
+    {
+        const u32 base = (lane * stride + 64u * q) >> 4;  // 64q + 64 <= total <= stride
+#pragma unroll
+        for (u32 c = 0; c < 4; c++)
+            lds[base + c] = make_uint4(D[4 * c], D[4 * c + 1], D[4 * c + 2], D[4 * c + 3]);
     }
     __device__ __forceinline__ void tag(const u32 t[4]) { lds[(lane * stride + 16u) >> 4] = make_uint4(t[0], t[1], t[2], t[3]); }
     __device__ __forceinline__ void finish()
@@ -359,7 +381,7 @@ __device__ __forceinline__ void seal_frame(const uint8_t *__restrict__ in, u32 n
         poly_block(P, C[4], C[5], C[6], C[7], 1u);
         poly_block(P, C[8], C[9], C[10], C[11], 1u);
         poly_block(P, C[12], C[13], C[14], C[15], 1u);
-        em.emit(blk, C);
+        em.emit_full(blk, C);
     };
 
     u32 carry;
@@ -504,7 +526,7 @@ __device__ __forceinline__ void seal_frame(const uint8_t *__restrict__ in, u32 n
             poly_block(P, C[4], C[5], C[6], C[7], 1u);
             poly_block(P, C[8], C[9], C[10], C[11], 1u);
             poly_block(P, C[12], C[13], C[14], C[15], 1u);
-            em.emit(blk, C);
+            em.emit_full(blk, C);
         }
     }
 
@@ -604,13 +626,16 @@ __device__ __forceinline__ u32 open_frame(const uint8_t *__restrict__ in, u32 si
     const u32 nfull = mlen >> 6;
     const u32 nout = (MODE == MODE_ZMQ) ? size - 33u : size;
 
-    auto emit_open = [&](u32 q, u32 D[16]) {
+    auto emit_open = [&](u32 q, u32 D[16], bool full) {
         if (COOP && dead) {
 #pragma unroll
             for (int k = 0; k < 16; k++)
                 D[k] = 0u;
         }
-        em.emit(q, D);
+        if (full)
+            em.emit_full(q, D);  // chunk q inside the output: no masking
+        else
+            em.emit(q, D);
     };
 
     u32 x[16], C[16], X[16];
@@ -655,7 +680,7 @@ __device__ __forceinline__ u32 open_frame(const uint8_t *__restrict__ in, u32 si
 #pragma unroll
             for (int k = 0; k < 8; k++)
                 X[k] = 0u;
-            emit_open(0, X);
+            emit_open(0, X, false);
         }
     }
 
@@ -691,12 +716,12 @@ __device__ __forceinline__ u32 open_frame(const uint8_t *__restrict__ in, u32 si
 #pragma unroll
             for (int t = 0; t < 16; t++)
                 O[t] = funnel(E[t + 1], E[t], 1);
-            emit_open(blk - 1, O);
+            emit_open(blk - 1, O, full);
 #pragma unroll
             for (int k = 0; k < 8; k++)
                 K[k] = X[8 + k];
         } else {
-            emit_open(blk, X);
+            emit_open(blk, X, full);
         }
     };
 
@@ -764,7 +789,7 @@ __device__ __forceinline__ u32 open_frame(const uint8_t *__restrict__ in, u32 si
 #pragma unroll
             for (int t = 0; t < 16; t++)
                 O[t] = t < 7 ? funnel(K[t + 1], K[t], 1) : (t == 7 ? funnel(0u, K[7], 1) : 0u);
-            emit_open(nblk - 1u, O);
+            emit_open(nblk - 1u, O, false);
         }
     }
 
@@ -879,6 +904,7 @@ struct EmitSegLines {
             flush(q >> 1);
         last_q = q;
     }
+    __device__ __forceinline__ void emit_full(u32 q, const u32 D[16]) { emit(q, D); }
     __device__ __forceinline__ void tag(const u32 t[4])
     {
         *reinterpret_cast<uint4 *>(mine + 16) = make_uint4(t[0], t[1], t[2], t[3]);

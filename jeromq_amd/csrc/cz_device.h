@@ -49,16 +49,18 @@ __device__ __forceinline__ void row_round(u32 x[16])
 // The 20 Salsa20 rounds with LAZY XORS (cz_salsa_lazy.h, generated and self-checked by
 // tools/gen_salsa_lazy.py).  Every int32 VALU instruction costs its SIMD 4 cycles on gfx950
 // whatever the opcode (tools/diag/salsa_ub.hip), so a block costs its instruction count.
-// Round 1 stays in C: its 3 wave-uniform quarter-rounds (constants, key, block counter, high
-// nonce word) go to the scalar unit.  Rounds 2..20 keep most `w ^= R` updates pending and let
-// v_xad_u32 ((a ^ b) + c) and v_bitop3_b32 (a ^ b ^ c) absorb them: 776 VALU instead of 912.
-// On return word w is x[w] ^ d[w] for the bits of CZ_LAZY_PENDING, x[w] otherwise.
-// -DCZ_SALSA_EAGER builds the plain rounds (A/B experiments).
+// Rounds 1-2 stay in C: with the key, constants, block counter and high nonce word
+// wave-uniform, the compiler moves 3 of round 1's quarter-rounds (and part of round 2) to
+// the scalar unit and reads uniform words as SGPR operands.  Rounds 3..20 keep most
+// `w ^= R` updates pending and let v_xad_u32 ((a ^ b) + c) and v_bitop3_b32 (a ^ b ^ c)
+// absorb them: 736 VALU instead of 864.  On return word w is x[w] ^ d[w] for the bits of
+// CZ_LAZY_PENDING, x[w] otherwise.  -DCZ_SALSA_EAGER builds the plain rounds (A/B).
+static_assert(CZ_LAZY_FIRST_ROUND == 3, "rounds_lazy runs rounds 1-2 in C");
 __device__ __forceinline__ void rounds_lazy(u32 x[16], u32 d[16])
 {
     col_round(x);
-#ifdef CZ_SALSA_EAGER
     row_round(x);
+#ifdef CZ_SALSA_EAGER
 #pragma unroll
     for (int i = 1; i < 10; i++) {
         col_round(x);
@@ -69,7 +71,7 @@ __device__ __forceinline__ void rounds_lazy(u32 x[16], u32 d[16])
         d[k] = 0u;
 #else
     u32 t0, t1, t2, t3;
-    asm(CZ_SALSA_R2_20_ASM
+    asm(CZ_SALSA_LAZY_ASM
         : "+v"(x[0]), "+v"(x[1]), "+v"(x[2]), "+v"(x[3]), "+v"(x[4]), "+v"(x[5]), "+v"(x[6]), "+v"(x[7]),
           "+v"(x[8]), "+v"(x[9]), "+v"(x[10]), "+v"(x[11]), "+v"(x[12]), "+v"(x[13]), "+v"(x[14]), "+v"(x[15]),
           "=&v"(d[0]), "=&v"(d[1]), "=&v"(d[2]), "=&v"(d[3]), "=&v"(d[4]), "=&v"(d[5]), "=&v"(d[6]), "=&v"(d[7]),

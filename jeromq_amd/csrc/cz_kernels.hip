@@ -52,12 +52,26 @@ enum Mode { MODE_ZMQ = 0, MODE_NACL = 1 };
 constexpr u32 HDR0 = 0x53454d07u, HDR1 = 0x45474153u;
 
 constexpr int BLOCK = 256;              // threads per workgroup (4 waves)
-// Build-time occupancy experiment knob (CZ_EXTRA_FLAGS=-DCZ_SEAL_WAVES_PER_EU=n): caps the VGPRs of
-// the uniform/segment kernels so that n waves fit per SIMD.
+// Build-time occupancy knobs (CZ_EXTRA_FLAGS): CZ_UNIFORM_WAVES_PER_EU=n caps the VGPRs of the
+// uniform seal/open kernels so that n waves fit per SIMD, CZ_SEG_WAVES_PER_EU=n the segment
+// kernel's; CZ_SEAL_WAVES_PER_EU=n sets both.
 #ifdef CZ_SEAL_WAVES_PER_EU
-#define CZ_OCC __attribute__((amdgpu_waves_per_eu(CZ_SEAL_WAVES_PER_EU, CZ_SEAL_WAVES_PER_EU)))
+#ifndef CZ_UNIFORM_WAVES_PER_EU
+#define CZ_UNIFORM_WAVES_PER_EU CZ_SEAL_WAVES_PER_EU
+#endif
+#ifndef CZ_SEG_WAVES_PER_EU
+#define CZ_SEG_WAVES_PER_EU CZ_SEAL_WAVES_PER_EU
+#endif
+#endif
+#ifdef CZ_UNIFORM_WAVES_PER_EU
+#define CZ_OCC __attribute__((amdgpu_waves_per_eu(CZ_UNIFORM_WAVES_PER_EU, CZ_UNIFORM_WAVES_PER_EU)))
 #else
 #define CZ_OCC
+#endif
+#ifdef CZ_SEG_WAVES_PER_EU
+#define CZ_SEG_OCC __attribute__((amdgpu_waves_per_eu(CZ_SEG_WAVES_PER_EU, CZ_SEG_WAVES_PER_EU)))
+#else
+#define CZ_SEG_OCC
 #endif
 constexpr int WAVES = BLOCK / 64;
 constexpr u32 LINE_LDS_BYTES = 64 * 128; // EmitLines: one 128-byte line per frame
@@ -1483,7 +1497,7 @@ __device__ __forceinline__ bool wave_lines_ok(bool full_wave, u32 nchunks, bool 
     return wave_uniform(nchunks) && __builtin_amdgcn_ballot_w64(!al) == 0;
 }
 
-__global__ __launch_bounds__(BLOCK) CZ_OCC void k_seal_segments(const cz_frame_desc *__restrict__ desc,
+__global__ __launch_bounds__(BLOCK) CZ_SEG_OCC void k_seal_segments(const cz_frame_desc *__restrict__ desc,
                                                           const cz_segment *__restrict__ segs, uint32_t nseg,
                                                           const uint8_t *__restrict__ in, uint8_t *__restrict__ out,
                                                           const uint8_t *__restrict__ subkeys,

@@ -1,5 +1,5 @@
 #!/usr/bin/env python3
-"""Generate jeromq_amd/csrc/cz_salsa_lazy.h: Salsa20 rounds 2..20 as one gfx950 inline-asm
+"""Generate jeromq_amd/csrc/cz_salsa_lazy.h: Salsa20 rounds 3..20 as one gfx950 inline-asm
 block with LAZY XORS (fewer VALU instructions per 64-byte block).
 
 Why.  On gfx950 every int32 VALU wave-instruction occupies its SIMD for 4 cycles,
@@ -14,10 +14,12 @@ So a word updated by `w ^= R` can keep R as a pending delta (0 instructions) as 
   * every add that reads it has at most one such lazy operand (v_xad_u32), and
   * it has at most one pending delta when updated again (then v_bitop3_b32 folds the
     old delta and the new R in one instruction).
-Which updates to defer is a small 0/1 program over the 16 words x 19 rounds (solved
-here with scipy's MILP): 168 fold/materialise instructions instead of 304 xors.  Round 1
-stays in C (the compiler moves its 3 wave-uniform quarter-rounds to the scalar unit);
-words left lazy after round 20 are absorbed by the feed-forward add (v_xad_u32).
+Which updates to defer is a small 0/1 program over the 16 words x 18 rounds (solved
+here with scipy's MILP): about half of the xors.  Rounds 1 and 2 stay in C: with the
+key, constants, block counter and high nonce word wave-uniform, the compiler moves 3 of
+round 1's quarter-rounds and part of round 2 to the scalar unit and reads the uniform
+words as SGPR operands (an asm block would need a v_mov per uniform word).  Words left
+lazy after round 20 are absorbed by the feed-forward add (v_xad_u32).
 
 Operands of the generated asm: %0..%15 state words m_w ("+v"), %16..%31 deltas d_w
 ("=&v"), %32..%35 temps ("=&v").  CZ_LAZY_PENDING has bit w set when d_w is pending at the
@@ -36,11 +38,12 @@ COL = [(0, 4, 8, 12), (5, 9, 13, 1), (10, 14, 2, 6), (15, 3, 7, 11)]
 ROW = [(0, 1, 2, 3), (5, 6, 7, 4), (10, 11, 8, 9), (15, 12, 13, 14)]
 ROT = [7, 9, 13, 18]
 W = 16
-ROUNDS = 19  # rounds 2..20 (round 2 is a row round)
+FIRST = 3   # first Salsa round (1-based) done in asm; rounds 1..FIRST-1 stay in C
+ROUNDS = 21 - FIRST
 
 
-def groups_of(r):  # r = 0..ROUNDS-1 <-> Salsa round r + 2
-    return ROW if r % 2 == 0 else COL
+def groups_of(r):  # r = 0..ROUNDS-1 <-> Salsa round r + FIRST (odd rounds are column rounds)
+    return COL if (r + FIRST) % 2 == 1 else ROW
 
 
 def solve():
@@ -187,8 +190,8 @@ def main():
     rng = random.Random(1)
     for _ in range(200):
         x = [rng.getrandbits(32) for _ in range(W)]
-        after1 = ref_rounds(x, 0, 1)
-        regs = after1 + [rng.getrandbits(32) for _ in range(20)]
+        before = ref_rounds(x, 0, FIRST - 1)
+        regs = before + [rng.getrandbits(32) for _ in range(20)]
         regs = interpret(lines, regs)
         got = [regs[w] ^ (regs[16 + w] if pend[w] else 0) for w in range(W)]
         assert got == ref_rounds(x, 0, 20), "lazy schedule mismatch"
@@ -200,14 +203,15 @@ def main():
     path = os.path.join(here, "..", "jeromq_amd", "csrc", "cz_salsa_lazy.h")
     body = " \\\n".join(f'    "{s}\\n"' for s in lines)
     hdr = f"""// cz_salsa_lazy.h -- GENERATED by tools/gen_salsa_lazy.py (do not edit).
-// Salsa20 rounds 2..20 with lazy xors: {len(lines)} VALU instructions
+// Salsa20 rounds {FIRST}..20 with lazy xors: {len(lines)} VALU instructions
 // ({", ".join(f"{k} {v}" for k, v in sorted(ops.items()))})
-// instead of 912 (19 rounds x 48).  Fold/materialise instructions: {cost} (vs 304 xors).
+// instead of {48 * ROUNDS} ({ROUNDS} rounds x 48).  Fold/materialise instructions: {cost} (vs {16 * ROUNDS} xors).
 // Operands: %0..%15 state m_w ("+v"), %16..%31 deltas d_w ("=&v"), %32..%35 temps ("=&v").
 // After the block, word w = m_w ^ d_w for every bit w of CZ_LAZY_PENDING, else m_w.
 #pragma once
 #define CZ_LAZY_PENDING 0x{mask:04x}u
-#define CZ_SALSA_R2_20_ASM \\
+#define CZ_LAZY_FIRST_ROUND {FIRST}
+#define CZ_SALSA_LAZY_ASM \\
 {body}
 """
     with open(path, "w") as f:

@@ -417,18 +417,34 @@ def beforenm_bench(args, dev):
                              "sample": "oracle/curve_oracle.c or_box_beforenm (radix 2^51), 2 s on 1 thread"}}
 
 
-def load_pmc_traffic(cfg):
-    """HBM bytes per launch from the committed rocprofv3 PMC summary, if one exists for this config."""
+def load_pmc(cfg):
+    """This config's entry of the committed rocprofv3 PMC summary (profiles/pmc_traffic.json:
+    HBM bytes per launch from tools/gpu_traffic.sh, VALU wave-instructions per launch from
+    tools/gpu_valu.sh), or {}."""
     path = os.path.join(ROOT, "profiles", "pmc_traffic.json")
-    if not os.path.exists(path):
-        return None
     try:
         with open(path) as f:
-            d = json.load(f)
-        v = d.get(cfg)
-        return None if v is None else float(v["hbm_bytes_per_launch"])
-    except Exception:
+            return json.load(f).get(cfg) or {}
+    except (OSError, ValueError):
+        return {}
+
+
+# VALU issue roofline.  Every int32 VALU wave-instruction occupies its SIMD for 4 cycles on
+# gfx950 (tools/diag/salsa_ub.hip, profiles/r01/ubench_salsa_issue.log: 3.9-4.1 cycles at 3-8
+# waves per SIMD, any opcode mix, any order), so the chip issues at most
+# 256 CUs x 4 SIMDs x 2.4 GHz / 4 = 614.4 G wave-instructions/s.
+VALU_PEAK_G = 256 * 4 * 2.4 / 4
+
+
+def valu_roofline(pmc, kernel_s):
+    n = pmc.get("valu_insts_per_launch")
+    if not n:
         return None
+    g = n / kernel_s / 1e9
+    return {"insts_per_launch": n, "achieved": round(g, 1), "peak": VALU_PEAK_G, "unit": "G wave-instr/s",
+            "frac": round(g / VALU_PEAK_G, 4),
+            "floor_ms_at_2.4GHz": round(n / (VALU_PEAK_G * 1e9) * 1e3, 4),
+            "source": pmc.get("valu_source")}
 
 
 def scatter_leg(wl, world, rank, dev):
@@ -525,7 +541,8 @@ def main():
     value = total_payload / elapsed / 2**30
     alg_bytes = wl.read_bytes + wl.write_bytes
     achieved = alg_bytes / avg_kernel_s / 1e9
-    traffic = load_pmc_traffic(args.config)
+    pmc = load_pmc(args.config)
+    traffic = pmc.get("hbm_bytes_per_launch")
 
     sg = None
     if world > 1 and args.config == "4k" and not args.no_scatter:
@@ -561,7 +578,9 @@ def main():
                          "frac": round(achieved / HBM_PEAK_GBS, 4),
                          "traffic": traffic,
                          "kernel_ms": round(avg_kernel_s * 1e3, 4),
-                         "alg_bytes_per_launch": alg_bytes},
+                         "alg_bytes_per_launch": alg_bytes,
+                         # the roof that binds: VALU issue
+                         "valu": valu_roofline(pmc, avg_kernel_s)},
             "cpu_baseline": cpu,
         }
         if sg is not None:

@@ -172,17 +172,19 @@ __device__ __forceinline__ void poly_block(Poly &P, u32 m0, u32 m1, u32 m2, u32 
     const u64 d3 = mad64(h4, P.s3, mad64(h3, P.r0, mad64(h2, P.r1, mad64(h1, P.r2, mad64(h0, P.r3, 0)))));
     const u32 h4r = h4 * P.r0;
 
-    // propagate the column carries: h = d0 + d1*2^32 + d2*2^64 + d3*2^96 + h4r*2^128
+    // propagate the column carries: h = d0 + d1*2^32 + d2*2^64 + d3*2^96 + h4r*2^128.
+    // One v_addc_co_u32 per limb: lo(d_j) + hi(d_{j-1}) + carry < 2^32 + 2^30.3 + 1, so
+    // the carry out is 0 or 1; hi(d3) + h4r + carry < 2^31 does not carry.
     const u32 e0 = (u32)d0;
     const u32 e1 = addc((u32)d1, (u32)(d0 >> 32), 0u, c);
-    u32 t = (u32)(d1 >> 32) + c;
-    const u32 e2 = addc((u32)d2, t, 0u, c);
-    t = (u32)(d2 >> 32) + c;
-    const u32 e3 = addc((u32)d3, t, 0u, c);
-    const u32 e4 = (u32)(d3 >> 32) + c + h4r;
+    const u32 e2 = addc((u32)d2, (u32)(d1 >> 32), c, c);
+    const u32 e3 = addc((u32)d3, (u32)(d2 >> 32), c, c);
+    const u32 e4 = addc((u32)(d3 >> 32), h4r, c, c);
     // partial reduction, 2^130 == 5: fold e4's bits above 2^130 back in
     const u32 q = e4 >> 2;
-    const u32 k = q + (q << 2);
+    // k = 5q as one v_lshl_add_u32: left to itself the compiler emits (e4 & ~3) + q, two VALU
+    u32 k;
+    asm("v_lshl_add_u32 %0, %1, 2, %1" : "=v"(k) : "v"(q));
     P.h0 = addc(e0, k, 0u, c);
     P.h1 = addc(e1, 0u, c, c);
     P.h2 = addc(e2, 0u, c, c);

@@ -103,6 +103,15 @@ __device__ __forceinline__ V4 ld16(const uint8_t *__restrict__ p, u64 avail)
     }
 }
 
+template <bool AL>
+__device__ __forceinline__ u32 ld32(const uint8_t *__restrict__ p)
+{
+    if constexpr (AL)
+        return *reinterpret_cast<const u32 *>(p);
+    else
+        return (u32)p[0] | ((u32)p[1] << 8) | ((u32)p[2] << 16) | ((u32)p[3] << 24);
+}
+
 // Unguarded full-chunk load (caller proved all 16 bytes valid).
 template <bool AL>
 __device__ __forceinline__ V4 ld16f(const uint8_t *__restrict__ p)
@@ -858,14 +867,6 @@ __device__ __forceinline__ u64 read_be64(const uint8_t *p)
 // at the loop's convergence point, so a wave whose lanes hold segments with
 // the same chunk count can share the cooperative line emitter below.
 // ---------------------------------------------------------------------------
-template <bool AL>
-__device__ __forceinline__ u32 ld32(const uint8_t *__restrict__ p)
-{
-    if constexpr (AL)
-        return *reinterpret_cast<const u32 *>(p);
-    else
-        return (u32)p[0] | ((u32)p[1] << 8) | ((u32)p[2] << 16) | ((u32)p[3] << 24);
-}
 
 // Line staging for a wave of segments at arbitrary 16-byte aligned bases.  Like
 // EmitLines, 8 lanes write one 128-byte output line per store instruction, but

@@ -69,6 +69,28 @@ __device__ __forceinline__ void rounds_lazy(u32 x[16], u32 d[16])
 #pragma unroll
     for (int k = 0; k < 16; k++)
         d[k] = 0u;
+#elif defined(CZ_SALSA_LAZY_SPLIT)
+    // one asm statement per round (same instructions): independent work can go in between
+    u32 t0, t1, t2, t3;
+#define CZ_LZ_X "+v"(x[0]), "+v"(x[1]), "+v"(x[2]), "+v"(x[3]), "+v"(x[4]), "+v"(x[5]), "+v"(x[6]), "+v"(x[7]), \
+                "+v"(x[8]), "+v"(x[9]), "+v"(x[10]), "+v"(x[11]), "+v"(x[12]), "+v"(x[13]), "+v"(x[14]), "+v"(x[15])
+#define CZ_LZ_T "=&v"(t0), "=&v"(t1), "=&v"(t2), "=&v"(t3)
+#define CZ_LZ_D(M) M(d[0]), M(d[1]), M(d[2]), M(d[3]), M(d[4]), M(d[5]), M(d[6]), M(d[7]), M(d[8]), M(d[9]), \
+                   M(d[10]), M(d[11]), M(d[12]), M(d[13]), M(d[14]), M(d[15])
+#define CZ_LZ_OUT(v) "=&v"(v)
+#define CZ_LZ_IO(v) "+v"(v)
+#define CZ_LZ_R(i) asm(CZ_SALSA_LAZY_ROUND_##i : CZ_LZ_X, CZ_LZ_D(CZ_LZ_IO), CZ_LZ_T)
+    asm(CZ_SALSA_LAZY_ROUND_0 : CZ_LZ_X, CZ_LZ_D(CZ_LZ_OUT), CZ_LZ_T);
+    CZ_LZ_R(1); CZ_LZ_R(2); CZ_LZ_R(3); CZ_LZ_R(4); CZ_LZ_R(5); CZ_LZ_R(6); CZ_LZ_R(7); CZ_LZ_R(8);
+    CZ_LZ_R(9); CZ_LZ_R(10); CZ_LZ_R(11); CZ_LZ_R(12); CZ_LZ_R(13); CZ_LZ_R(14); CZ_LZ_R(15); CZ_LZ_R(16);
+    CZ_LZ_R(17);
+    static_assert(CZ_LAZY_FIRST_ROUND + 17 == 20, "per-round list covers rounds 3..20");
+#undef CZ_LZ_R
+#undef CZ_LZ_IO
+#undef CZ_LZ_OUT
+#undef CZ_LZ_D
+#undef CZ_LZ_T
+#undef CZ_LZ_X
 #else
     u32 t0, t1, t2, t3;
     asm(CZ_SALSA_LAZY_ASM
@@ -89,20 +111,40 @@ __device__ __forceinline__ constexpr bool lazy_pending(int k)
 #endif
 }
 
+// The 20 rounds with plain xors (compiler-scheduled).
+__device__ __forceinline__ void rounds_eager(u32 x[16])
+{
+#pragma unroll
+    for (int i = 0; i < 10; i++) {
+        col_round(x);
+        row_round(x);
+    }
+}
+
 // One Salsa20/20 block: key k[8] (LE words), nonce words n0,n1 (LE loads of
 // nonce bytes 16..23 of the XSalsa20 nonce), 64-bit block counter c0|c1.
-// The feed-forward add absorbs the deltas rounds_lazy left pending (v_xad_u32).
+// LAZY: rounds_lazy, whose pending deltas the feed-forward add absorbs (v_xad_u32).
+// The lane-per-frame descriptor kernels take the plain rounds: on their ragged,
+// tail-latency-bound batches the lazy core measured 9% slower.
+template <bool LAZY = true>
 __device__ __forceinline__ void salsa20_block(u32 x[16], const u32 k[8], u32 n0, u32 n1, u32 c0, u32 c1)
 {
     const u32 in[16] = {SIGMA0, k[0], k[1], k[2], k[3], SIGMA1, n0, n1, c0, c1, SIGMA2, k[4], k[5], k[6], k[7], SIGMA3};
-    u32 d[16];
 #pragma unroll
     for (int i = 0; i < 16; i++)
         x[i] = in[i];
-    rounds_lazy(x, d);
+    if constexpr (LAZY) {
+        u32 d[16];
+        rounds_lazy(x, d);
 #pragma unroll
-    for (int i = 0; i < 16; i++)
-        x[i] = lazy_pending(i) ? ((x[i] ^ d[i]) + in[i]) : (x[i] + in[i]);
+        for (int i = 0; i < 16; i++)
+            x[i] = lazy_pending(i) ? ((x[i] ^ d[i]) + in[i]) : (x[i] + in[i]);
+    } else {
+        rounds_eager(x);
+#pragma unroll
+        for (int i = 0; i < 16; i++)
+            x[i] += in[i];
+    }
 }
 
 // HSalsa20(k, in16) -> out[8]: no feed-forward, words 0,5,10,15,6,7,8,9.

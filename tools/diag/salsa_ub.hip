@@ -122,8 +122,10 @@ constexpr int MAXK = 8;
 template <int V>
 void run(const char *name, int k, int nb)
 {
-    const int lds = (160 * 1024 / k) & ~255;
-    const int blocks = 256 * k * ROUNDS;
+    // k <= 2: one round of 256 x k workgroups and no LDS (64 KiB is the dynamic-LDS cap);
+    // the dispatcher spreads them one per CU per k
+    const int lds = k <= 2 ? 0 : (160 * 1024 / k) & ~255;
+    const int blocks = k <= 2 ? 256 * k : 256 * k * ROUNDS;
     hipEvent_t e0, e1;
     CK(hipEventCreate(&e0));
     CK(hipEventCreate(&e1));
@@ -158,7 +160,7 @@ void run(const char *name, int k, int nb)
             ghz.push_back((double)h[2 * w] / (double)h[2 * w + 1] * 0.1);
     std::sort(ghz.begin(), ghz.end());
     const double clock = ghz.empty() ? 0.0 : ghz[ghz.size() / 2];
-    const double wave_blocks_per_simd = (double)nw * nb / 1024.0;
+    const double wave_blocks_per_simd = (double)nw * nb / 1024.0;  // k <= 2: ~k waves on every SIMD
     const double cyc = ms * 1e-3 * clock * 1e9 / wave_blocks_per_simd;
     printf("%-13s k=%d  %8.3f ms  clock %.2f GHz  %6.0f SIMD-cycles/wave-block  %.3f per double-round VALU\n", name,
            k, ms, clock, cyc, cyc / 960.0);
@@ -176,7 +178,16 @@ int main(int argc, char **argv)
     const u32 hk[8] = {0x1c0cdcc8u, 0x5efe8027u, 0x003e7ec2u, 0xb2b2ff1au,
                        0x15f329a9u, 0x96b142a6u, 0xc4db132cu, 0x6fd51f90u};
     CK(hipMemcpy(d_key, hk, 32, hipMemcpyHostToDevice));
-    for (int k : {4, 3, 5, 6, 8}) {
+    const char *ks = getenv("UB_WAVES");
+    std::vector<int> kv;
+    if (ks) {
+        for (const char *c = ks; *c; c++)
+            if (*c >= '1' && *c <= '8')
+                kv.push_back(*c - '0');
+    } else {
+        kv = {4, 3, 5, 6, 8};
+    }
+    for (int k : kv) {
         run<C_SALSA>("c_salsa", k, nb);
         run<C_SALSA_POLY>("c_salsa_poly", k, nb);
         run<A_GROUPED>("a_grouped", k, nb);

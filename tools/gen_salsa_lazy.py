@@ -97,6 +97,7 @@ def emit(A, F):
     tmp = lambda i: f"%{32 + i}"  # noqa: E731
     pend = [0] * W
     out = []
+    starts = []  # index of each round's first instruction
 
     def val(w):  # operand list of word w's current value: (m,) or (m, d)
         return (m(w), d(w)) if pend[w] else (m(w),)
@@ -113,6 +114,7 @@ def emit(A, F):
 
     for r in range(ROUNDS):
         groups = groups_of(r)
+        starts.append(len(out))
         # materialise at round start where the schedule clears a pending delta without a fold
         for w in range(W):
             if pend[w] and not A[r][w]:
@@ -139,7 +141,7 @@ def emit(A, F):
                 else:
                     assert not pend[dst] and reg == d(dst), "deferred update on a pending word"
                     pend[dst] = 1
-    return out, pend
+    return out, pend, starts
 
 
 # ---------------------------------------------------------------------------- check
@@ -186,7 +188,7 @@ def interpret(lines, regs):
 
 def main():
     A, F, cost = solve()
-    lines, pend = emit(A, F)
+    lines, pend, starts = emit(A, F)
     rng = random.Random(1)
     for _ in range(200):
         x = [rng.getrandbits(32) for _ in range(W)]
@@ -202,6 +204,10 @@ def main():
     here = os.path.dirname(os.path.abspath(__file__))
     path = os.path.join(here, "..", "jeromq_amd", "csrc", "cz_salsa_lazy.h")
     body = " \\\n".join(f'    "{s}\\n"' for s in lines)
+    bounds = starts + [len(lines)]
+    rounds = "\n".join(
+        f"#define CZ_SALSA_LAZY_ROUND_{i} \\\n" + " \\\n".join(f'    "{s}\\n"' for s in lines[bounds[i]:bounds[i + 1]])
+        for i in range(ROUNDS))
     hdr = f"""// cz_salsa_lazy.h -- GENERATED by tools/gen_salsa_lazy.py (do not edit).
 // Salsa20 rounds {FIRST}..20 with lazy xors: {len(lines)} VALU instructions
 // ({", ".join(f"{k} {v}" for k, v in sorted(ops.items()))})
@@ -213,6 +219,10 @@ def main():
 #define CZ_LAZY_FIRST_ROUND {FIRST}
 #define CZ_SALSA_LAZY_ASM \\
 {body}
+
+// The same instructions one Salsa20 round per macro (rounds {FIRST}..20), so the compiler can
+// place independent work (the previous block's Poly1305, loads, stores) between rounds.
+{rounds}
 """
     with open(path, "w") as f:
         f.write(hdr)

@@ -46,6 +46,49 @@ __device__ __forceinline__ void row_round(u32 x[16])
     qr(x[15], x[12], x[13], x[14]);
 }
 
+// rotl of a WAVE-UNIFORM value on the scalar unit.  Left to itself the compiler rotates
+// uniform values with v_alignbit_b32 (there is no scalar rotate), which moves everything
+// downstream to the VALU; 3 SALU instructions cost the VALU nothing.  Only call with
+// values that are the same in every lane: an "s" operand of a divergent value would be
+// silently narrowed to lane 0.
+template <int C>
+__device__ __forceinline__ u32 srotl(u32 v)
+{
+    u32 r, t;
+    asm("s_lshl_b32 %0, %2, %3\n\ts_lshr_b32 %1, %2, %4\n\ts_or_b32 %0, %0, %1"
+        : "=&s"(r), "=&s"(t)
+        : "s"(v), "i"(C), "i"(32 - C)
+        : "scc");
+    return r;
+}
+
+// Rounds 1-2 when the key, the block counter and nonce word 6 are wave-uniform and only
+// word 7 (the low counter word of a MESSAGE nonce) differs per lane.  Every rotate whose
+// input is uniform goes to the scalar unit: round 1's quarter-rounds A, B, C and half of D,
+// round 2's A and one step each of B and C.  The per-lane rest is 27 VALU instead of ~48
+// (the compiler still hoists the per-frame-invariant part out of the block loop).
+__device__ __forceinline__ void rounds12_uniform(u32 x[16])
+{
+    // round 1 (columns)
+    x[4] ^= srotl<7>(x[0] + x[12]);  x[8] ^= srotl<9>(x[4] + x[0]);
+    x[12] ^= srotl<13>(x[8] + x[4]); x[0] ^= srotl<18>(x[12] + x[8]);
+    x[9] ^= srotl<7>(x[5] + x[1]);   x[13] ^= srotl<9>(x[9] + x[5]);
+    x[1] ^= srotl<13>(x[13] + x[9]); x[5] ^= srotl<18>(x[1] + x[13]);
+    x[14] ^= srotl<7>(x[10] + x[6]); x[2] ^= srotl<9>(x[14] + x[10]);
+    x[6] ^= srotl<13>(x[2] + x[14]); x[10] ^= srotl<18>(x[6] + x[2]);
+    x[3] ^= srotl<7>(x[15] + x[11]); x[7] ^= srotl<9>(x[3] + x[15]);   // x7 per-lane from here
+    x[11] ^= rotl(x[7] + x[3], 13);  x[15] ^= rotl(x[11] + x[7], 18);
+    // round 2 (rows)
+    x[1] ^= srotl<7>(x[0] + x[3]);   x[2] ^= srotl<9>(x[1] + x[0]);
+    x[3] ^= srotl<13>(x[2] + x[1]);  x[0] ^= srotl<18>(x[3] + x[2]);
+    x[6] ^= srotl<7>(x[5] + x[4]);   x[7] ^= srotl<9>(x[6] + x[5]);
+    x[4] ^= rotl(x[7] + x[6], 13);   x[5] ^= rotl(x[4] + x[7], 18);
+    x[11] ^= srotl<7>(x[10] + x[9]); x[8] ^= rotl(x[11] + x[10], 9);
+    x[9] ^= rotl(x[8] + x[11], 13);  x[10] ^= rotl(x[9] + x[8], 18);
+    x[12] ^= rotl(x[15] + x[14], 7); x[13] ^= rotl(x[12] + x[15], 9);
+    x[14] ^= rotl(x[13] + x[12], 13); x[15] ^= rotl(x[14] + x[13], 18);
+}
+
 // The 20 Salsa20 rounds with LAZY XORS (cz_salsa_lazy.h, generated and self-checked by
 // tools/gen_salsa_lazy.py).  Every int32 VALU instruction costs its SIMD 4 cycles on gfx950
 // whatever the opcode (tools/diag/salsa_ub.hip), so a block costs its instruction count.
@@ -55,11 +98,17 @@ __device__ __forceinline__ void row_round(u32 x[16])
 // `w ^= R` updates pending and let v_xad_u32 ((a ^ b) + c) and v_bitop3_b32 (a ^ b ^ c)
 // absorb them: 736 VALU instead of 864.  On return word w is x[w] ^ d[w] for the bits of
 // CZ_LAZY_PENDING, x[w] otherwise.  -DCZ_SALSA_EAGER builds the plain rounds (A/B).
+// UNI: the caller guarantees rounds12_uniform's precondition (UN0 kernels).
 static_assert(CZ_LAZY_FIRST_ROUND == 3, "rounds_lazy runs rounds 1-2 in C");
+template <bool UNI = false>
 __device__ __forceinline__ void rounds_lazy(u32 x[16], u32 d[16])
 {
-    col_round(x);
-    row_round(x);
+    if constexpr (UNI) {
+        rounds12_uniform(x);
+    } else {
+        col_round(x);
+        row_round(x);
+    }
 #ifdef CZ_SALSA_EAGER
 #pragma unroll
     for (int i = 1; i < 10; i++) {
@@ -126,7 +175,8 @@ __device__ __forceinline__ void rounds_eager(u32 x[16])
 // LAZY: rounds_lazy, whose pending deltas the feed-forward add absorbs (v_xad_u32).
 // The lane-per-frame descriptor kernels take the plain rounds: on their ragged,
 // tail-latency-bound batches the lazy core measured 9% slower.
-template <bool LAZY = true>
+// UNI: key, n0, c0, c1 are wave-uniform (the UN0 kernels), see rounds12_uniform.
+template <bool LAZY = true, bool UNI = false>
 __device__ __forceinline__ void salsa20_block(u32 x[16], const u32 k[8], u32 n0, u32 n1, u32 c0, u32 c1)
 {
     const u32 in[16] = {SIGMA0, k[0], k[1], k[2], k[3], SIGMA1, n0, n1, c0, c1, SIGMA2, k[4], k[5], k[6], k[7], SIGMA3};
@@ -135,7 +185,7 @@ __device__ __forceinline__ void salsa20_block(u32 x[16], const u32 k[8], u32 n0,
         x[i] = in[i];
     if constexpr (LAZY) {
         u32 d[16];
-        rounds_lazy(x, d);
+        rounds_lazy<UNI>(x, d);
 #pragma unroll
         for (int i = 0; i < 16; i++)
             x[i] = lazy_pending(i) ? ((x[i] ^ d[i]) + in[i]) : (x[i] + in[i]);

@@ -63,27 +63,46 @@ __device__ __forceinline__ u32 srotl(u32 v)
 }
 
 // Rounds 1-2 when the key, the block counter and nonce word 6 are wave-uniform and only
-// word 7 (the low counter word of a MESSAGE nonce) differs per lane.  Every rotate whose
-// input is uniform goes to the scalar unit: round 1's quarter-rounds A, B, C and half of D,
-// round 2's A and one step each of B and C.  The per-lane rest is 27 VALU instead of ~48
-// (the compiler still hoists the per-frame-invariant part out of the block loop).
-__device__ __forceinline__ void rounds12_uniform(u32 x[16])
+// word 7 (the low counter word of a MESSAGE nonce) differs per lane (the UN0 kernels).
+// Round 1's quarter-rounds B, C, D do not depend on the block counter: salsa_frame()
+// runs them once per frame.  Per block, what depends on the block counter and is
+// wave-uniform -- round 1's A, round 2's A and the first step of round 2's B -- rotates on
+// the scalar unit (srotl); the per-lane rest is ~24 VALU.
+struct SalsaFrame {
+    u32 w[16];  // state after round 1's quarter-rounds B, C, D (words 0, 4, 8, 12 unused)
+};
+
+__device__ __forceinline__ SalsaFrame salsa_frame(const u32 k[8], u32 n0, u32 n1)
 {
-    // round 1 (columns)
-    x[4] ^= srotl<7>(x[0] + x[12]);  x[8] ^= srotl<9>(x[4] + x[0]);
-    x[12] ^= srotl<13>(x[8] + x[4]); x[0] ^= srotl<18>(x[12] + x[8]);
+    u32 x[16] = {SIGMA0, k[0], k[1], k[2], k[3], SIGMA1, n0, n1, 0u, 0u, SIGMA2, k[4], k[5], k[6], k[7], SIGMA3};
     x[9] ^= srotl<7>(x[5] + x[1]);   x[13] ^= srotl<9>(x[9] + x[5]);
     x[1] ^= srotl<13>(x[13] + x[9]); x[5] ^= srotl<18>(x[1] + x[13]);
     x[14] ^= srotl<7>(x[10] + x[6]); x[2] ^= srotl<9>(x[14] + x[10]);
     x[6] ^= srotl<13>(x[2] + x[14]); x[10] ^= srotl<18>(x[6] + x[2]);
     x[3] ^= srotl<7>(x[15] + x[11]); x[7] ^= srotl<9>(x[3] + x[15]);   // x7 per-lane from here
     x[11] ^= rotl(x[7] + x[3], 13);  x[15] ^= rotl(x[11] + x[7], 18);
+    SalsaFrame f;
+#pragma unroll
+    for (int i = 0; i < 16; i++)
+        f.w[i] = x[i];
+    return f;
+}
+
+// rounds 1-2 of block c0 (block counter high word 0) from the frame's precomputed words
+__device__ __forceinline__ void rounds12_frame(u32 x[16], const SalsaFrame &f, u32 c0, const u32 k[8])
+{
+#pragma unroll
+    for (int i = 0; i < 16; i++)
+        x[i] = f.w[i];
+    x[0] = SIGMA0; x[4] = k[3]; x[8] = c0; x[12] = k[5];
+    x[4] ^= srotl<7>(x[0] + x[12]);  x[8] ^= srotl<9>(x[4] + x[0]);
+    x[12] ^= srotl<13>(x[8] + x[4]); x[0] ^= srotl<18>(x[12] + x[8]);
     // round 2 (rows)
     x[1] ^= srotl<7>(x[0] + x[3]);   x[2] ^= srotl<9>(x[1] + x[0]);
     x[3] ^= srotl<13>(x[2] + x[1]);  x[0] ^= srotl<18>(x[3] + x[2]);
     x[6] ^= srotl<7>(x[5] + x[4]);   x[7] ^= srotl<9>(x[6] + x[5]);
     x[4] ^= rotl(x[7] + x[6], 13);   x[5] ^= rotl(x[4] + x[7], 18);
-    x[11] ^= srotl<7>(x[10] + x[9]); x[8] ^= rotl(x[11] + x[10], 9);
+    x[11] ^= rotl(x[10] + x[9], 7);  x[8] ^= rotl(x[11] + x[10], 9);
     x[9] ^= rotl(x[8] + x[11], 13);  x[10] ^= rotl(x[9] + x[8], 18);
     x[12] ^= rotl(x[15] + x[14], 7); x[13] ^= rotl(x[12] + x[15], 9);
     x[14] ^= rotl(x[13] + x[12], 13); x[15] ^= rotl(x[14] + x[13], 18);
@@ -98,14 +117,12 @@ __device__ __forceinline__ void rounds12_uniform(u32 x[16])
 // `w ^= R` updates pending and let v_xad_u32 ((a ^ b) + c) and v_bitop3_b32 (a ^ b ^ c)
 // absorb them: 736 VALU instead of 864.  On return word w is x[w] ^ d[w] for the bits of
 // CZ_LAZY_PENDING, x[w] otherwise.  -DCZ_SALSA_EAGER builds the plain rounds (A/B).
-// UNI: the caller guarantees rounds12_uniform's precondition (UN0 kernels).
+// R12: rounds 1-2 already done by the caller (rounds12_frame).
 static_assert(CZ_LAZY_FIRST_ROUND == 3, "rounds_lazy runs rounds 1-2 in C");
-template <bool UNI = false>
+template <bool R12 = false>
 __device__ __forceinline__ void rounds_lazy(u32 x[16], u32 d[16])
 {
-    if constexpr (UNI) {
-        rounds12_uniform(x);
-    } else {
+    if constexpr (!R12) {
         col_round(x);
         row_round(x);
     }
@@ -175,8 +192,7 @@ __device__ __forceinline__ void rounds_eager(u32 x[16])
 // LAZY: rounds_lazy, whose pending deltas the feed-forward add absorbs (v_xad_u32).
 // The lane-per-frame descriptor kernels take the plain rounds: on their ragged,
 // tail-latency-bound batches the lazy core measured 9% slower.
-// UNI: key, n0, c0, c1 are wave-uniform (the UN0 kernels), see rounds12_uniform.
-template <bool LAZY = true, bool UNI = false>
+template <bool LAZY = true>
 __device__ __forceinline__ void salsa20_block(u32 x[16], const u32 k[8], u32 n0, u32 n1, u32 c0, u32 c1)
 {
     const u32 in[16] = {SIGMA0, k[0], k[1], k[2], k[3], SIGMA1, n0, n1, c0, c1, SIGMA2, k[4], k[5], k[6], k[7], SIGMA3};
@@ -185,7 +201,7 @@ __device__ __forceinline__ void salsa20_block(u32 x[16], const u32 k[8], u32 n0,
         x[i] = in[i];
     if constexpr (LAZY) {
         u32 d[16];
-        rounds_lazy<UNI>(x, d);
+        rounds_lazy(x, d);
 #pragma unroll
         for (int i = 0; i < 16; i++)
             x[i] = lazy_pending(i) ? ((x[i] ^ d[i]) + in[i]) : (x[i] + in[i]);
@@ -195,6 +211,20 @@ __device__ __forceinline__ void salsa20_block(u32 x[16], const u32 k[8], u32 n0,
         for (int i = 0; i < 16; i++)
             x[i] += in[i];
     }
+}
+
+// The same block in a UN0 kernel (key, n0 and the block counter wave-uniform; c1 = 0),
+// rounds 1-2 from the frame's precomputed words (salsa_frame).
+__device__ __forceinline__ void salsa20_block_frame(u32 x[16], const SalsaFrame &f, const u32 k[8], u32 n0, u32 n1,
+                                                    u32 c0)
+{
+    const u32 in[16] = {SIGMA0, k[0], k[1], k[2], k[3], SIGMA1, n0, n1, c0, 0u, SIGMA2, k[4], k[5], k[6], k[7], SIGMA3};
+    u32 d[16];
+    rounds12_frame(x, f, c0, k);
+    rounds_lazy<true>(x, d);
+#pragma unroll
+    for (int i = 0; i < 16; i++)
+        x[i] = lazy_pending(i) ? ((x[i] ^ d[i]) + in[i]) : (x[i] + in[i]);
 }
 
 // HSalsa20(k, in16) -> out[8]: no feed-forward, words 0,5,10,15,6,7,8,9.

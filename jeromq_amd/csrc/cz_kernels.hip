@@ -389,14 +389,24 @@ __device__ __forceinline__ void seal_frame(const uint8_t *__restrict__ in, u32 n
     if constexpr (UN0)
         n0 = __builtin_amdgcn_readfirstlane(n0);
 
+    // keystream block c0 (c1 = 0): UN0 kernels take rounds 1-2 from the per-frame words
+    [[maybe_unused]] SalsaFrame sf{};
+    if constexpr (UN0 && LAZY)
+        sf = salsa_frame(key, n0, n1);
+    auto ksblock = [&](u32 *xs, u32 c0, u32 c1) {
+        if constexpr (UN0 && LAZY)
+            salsa20_block_frame(xs, sf, key, n0, n1, c0);
+        else
+            salsa20_block<LAZY>(xs, key, n0, n1, c0, c1);
+    };
     u32 x[16], C[16];
-    salsa20_block<LAZY, UN0>(x, key, n0, n1, 0u, 0u);
+    ksblock(x, 0u, 0u);
     Poly P;
     poly_init(P, x[0], x[1], x[2], x[3], x[4], x[5], x[6], x[7]);
 
     // ZMQ, one full block b >= 1 from its 17-dword window W = P[16b-9 .. 16b+7]
     auto zmq_full_block = [&](u32 blk, const u32 *W) {
-        salsa20_block<LAZY, UN0>(x, key, n0, n1, blk, 0u);
+        ksblock(x, blk, 0u);
 #pragma unroll
         for (int k = 0; k < 16; k++)
             C[k] = funnel(W[k + 1], W[k], 3) ^ x[k];
@@ -539,7 +549,7 @@ __device__ __forceinline__ void seal_frame(const uint8_t *__restrict__ in, u32 n
             q1 = ld16f<AL>(src + 16);
             q2 = ld16f<AL>(src + 32);
             q3 = ld16f<AL>(src + 48);
-            salsa20_block<LAZY, UN0>(x, key, n0, n1, blk, 0u);
+            ksblock(x, blk, 0u);
             u32 W[16] = {q0.x, q0.y, q0.z, q0.w, q1.x, q1.y, q1.z, q1.w,
                          q2.x, q2.y, q2.z, q2.w, q3.x, q3.y, q3.z, q3.w};
 #pragma unroll
@@ -563,7 +573,7 @@ __device__ __forceinline__ void seal_frame(const uint8_t *__restrict__ in, u32 n
             u64 avail = (o >= 0 && (u64)o < inlen) ? inlen - (u64)o : 0;
             q[c] = ld16<AL>(in + o, avail);
         }
-        salsa20_block<LAZY, UN0>(x, key, n0, n1, blk, 0u);
+        ksblock(x, blk, 0u);
         u32 W[16] = {q[0].x, q[0].y, q[0].z, q[0].w, q[1].x, q[1].y, q[1].z, q[1].w,
                      q[2].x, q[2].y, q[2].z, q[2].w, q[3].x, q[3].y, q[3].z, q[3].w};
         if constexpr (MODE == MODE_ZMQ) {
@@ -643,6 +653,16 @@ __device__ __forceinline__ u32 open_frame(const uint8_t *__restrict__ in, u32 si
     const bool dead = early != CZ_STATUS_OK;
     if constexpr (UN0)
         n0 = __builtin_amdgcn_readfirstlane(n0);  // caller checked: same in every lane
+    // keystream block c0 (c1 = 0): UN0 kernels take rounds 1-2 from the per-frame words
+    [[maybe_unused]] SalsaFrame sf{};
+    if constexpr (UN0 && LAZY)
+        sf = salsa_frame(key, n0, n1);
+    auto ksblock = [&](u32 *xs, u32 c0, u32 c1) {
+        if constexpr (UN0 && LAZY)
+            salsa20_block_frame(xs, sf, key, n0, n1, c0);
+        else
+            salsa20_block<LAZY>(xs, key, n0, n1, c0, c1);
+    };
 
     const u32 mlen = size;
     const u32 nblk = (mlen + 63u) >> 6;
@@ -662,7 +682,7 @@ __device__ __forceinline__ u32 open_frame(const uint8_t *__restrict__ in, u32 si
     };
 
     u32 x[16], C[16], X[16];
-    salsa20_block<LAZY, UN0>(x, key, n0, n1, 0u, 0u);
+    ksblock(x, 0u, 0u);
     Poly P;
     poly_init(P, x[0], x[1], x[2], x[3], x[4], x[5], x[6], x[7]);
     V4 tin = ld16<AL>(in + 16, size - 16u);
@@ -709,7 +729,7 @@ __device__ __forceinline__ u32 open_frame(const uint8_t *__restrict__ in, u32 si
 
     // one block b >= 1 whose 64 ciphertext bytes are in C (full: all 64 valid)
     auto open_block = [&](u32 blk, bool full) {
-        salsa20_block<LAZY, UN0>(x, key, n0, n1, blk, 0u);
+        ksblock(x, blk, 0u);
         if (full) {
             poly_block(P, C[0], C[1], C[2], C[3], 1u);
             poly_block(P, C[4], C[5], C[6], C[7], 1u);

@@ -292,6 +292,38 @@ def test_uniform_seal_open_vs_oracle(torch_dev, subkeys, n, in_stride, out_strid
     assert np.array_equal(plain, hin[:count * in_stride].reshape(count, in_stride)[:, :n])
 
 
+# Nonce counters whose high 32-bit word changes inside a wave (2^32 - 100: waves straddle the
+# boundary and take the per-lane path) or is uniform but nonzero (2^32 + 7, 2^48 + 3).  The
+# uniform kernels move wave-uniform Salsa20 work to the scalar unit only when the high word
+# is the same in every lane (cz_device.h rounds12_uniform), so both paths are compared here.
+@pytest.mark.parametrize("counter0", [2**32 - 100, 2**32 + 7, 2**48 + 3])
+@pytest.mark.parametrize("n,in_stride,out_stride,count", [(4096, 4096, 4224, 1024 + 64), (100, 112, 144, 2048)])
+def test_uniform_counter_high_word(torch_dev, subkeys, n, in_stride, out_stride, count, counter0):
+    torch, dev = torch_dev
+    from jeromq_amd import batch
+    d_in = torch.empty(count * in_stride, dtype=torch.uint8, device=dev)
+    batch.fill(d_in, 0x5EED1000 + n)
+    flags = torch.zeros(count, dtype=torch.uint8, device=dev)
+    flags[::8] = 1
+    d_out = torch.full((count * out_stride,), 0xAB, dtype=torch.uint8, device=dev)
+    batch.seal_uniform(d_in, in_stride, d_out, out_stride, count, n, subkeys[0], counter0, flags8=flags)
+    torch.cuda.synchronize()
+    hin = d_in.cpu().numpy()
+    fl = flags.cpu().numpy()
+    want = _oracle_uniform(hin, in_stride, count, n, fl, counter0)
+    got = d_out.cpu().numpy().reshape(count, out_stride)[:, :n + 33]
+    bad = np.nonzero(np.any(got != want, axis=1))[0]
+    assert len(bad) == 0, f"{len(bad)} frames differ, first {bad[:5]}"
+    d_plain = torch.zeros(count * in_stride, dtype=torch.uint8, device=dev)
+    status = torch.full((count,), -1, dtype=torch.int16, device=dev)
+    batch.open_uniform(d_out, out_stride, d_plain, in_stride, count, n + 33, subkeys[0], counter0 - 1, status)
+    torch.cuda.synchronize()
+    st = status.cpu().numpy().view(np.uint16)
+    assert np.all(st & 0xff == 0)
+    plain = d_plain.cpu().numpy().reshape(count, in_stride)[:, :n]
+    assert np.array_equal(plain, hin.reshape(count, in_stride)[:, :n])
+
+
 @pytest.mark.parametrize("n,body_stride,pay_stride", [(4096, 4224, 4096), (100, 144, 112), (1000, 1040, 1008)])
 def test_uniform_open_rejections_in_a_full_wave(torch_dev, subkeys, L, n, body_stride, pay_stride):
     """Rejected frames inside a cooperative (LDS-staged) wave: statuses per frame, the

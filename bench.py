@@ -12,7 +12,9 @@ frame MORE.  Payload bytes: counter-based SplitMix64, generated on device.
 
 N > 1 (torch.distributed.run, one rank per GPU): every rank seals its own 2^20
 frames (counters offset by rank * 2^20): no collective on the timed path ("weak").
-Rank 0 prints ONE JSON line.  `value` = payload GiB/s over all ranks.
+Rank 0 prints ONE JSON line.  `value` = payload GiB/s over all ranks.  The 4k line also
+carries `seal_open_verify` (configs[4]: seal, then open + tag-verify of the same frames, timed
+apart from `value`) and, at N > 1, `scatter_gather` (RCCL scatter -> seal -> gather).
 """
 import argparse
 import ctypes
@@ -52,6 +54,8 @@ def parse():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-scatter", action="store_true",
                     help="N>1, 4k: skip the separately timed RCCL scatter -> seal -> gather leg")
+    ap.add_argument("--no-roundtrip", action="store_true",
+                    help="4k: skip the separately timed seal -> open+verify leg (BASELINE.json configs[4])")
     ap.add_argument("--cpu-seconds", type=float, default=10.0, help="target CPU-baseline sample duration")
     return ap.parse_args()
 
@@ -497,6 +501,35 @@ def scatter_leg(wl, world, rank, dev):
             "e2e_GiBps": round(total_payload / (t_sc + t_seal + t_ga) / 2**30, 3), "verified": bool(verified)}
 
 
+def roundtrip_leg(wl, world, steps):
+    """BASELINE.json configs[4]: every rank seals its 2^20 x 4 KiB shard and
+    opens + tag-verifies the bodies it just sealed (CurveServerMechanism.decode, nonce strictly
+    above the previous one), timed separately from `value` with the same barrier + max-over-ranks
+    clock.  `verified`: every status is OK and every opened payload equals its input, on all ranks."""
+    plain = torch.empty_like(wl.d_in)
+    status = torch.empty(wl.count, dtype=torch.int16, device=wl.dev)
+
+    def rt():
+        wl.step()
+        batch.open_uniform(wl.d_out, wl.out_stride, plain, wl.in_stride, wl.count, wl.n + 33, wl.subkey,
+                           wl.counter0 - 1, status)
+    for _ in range(3):
+        rt()
+    torch.cuda.synchronize()
+    barrier(world)
+    t0 = time.perf_counter()
+    for _ in range(steps):
+        rt()
+    torch.cuda.synchronize()
+    barrier(world)
+    elapsed = max_over_ranks(world, time.perf_counter() - t0)
+    ok = not bool((status & 0xff).any().item()) and torch.equal(plain, wl.d_in)  # low byte: rc, high: flags
+    ok = sum_over_ranks(world, 1.0 if ok else 0.0) == world
+    total = sum_over_ranks(world, float(wl.payload_bytes)) * steps
+    return {"steps": steps, "ms_per_roundtrip": round(elapsed / steps * 1e3, 4),
+            "payload_GiBps": round(total / elapsed / 2**30, 3), "verified": bool(ok)}
+
+
 def main():
     args = parse()
     world, rank, local = setup_dist(args)
@@ -548,6 +581,10 @@ def main():
     if world > 1 and args.config == "4k" and not args.no_scatter:
         sg = scatter_leg(wl, world, rank, dev)
 
+    rtl = None
+    if args.config == "4k" and not args.no_roundtrip:
+        rtl = roundtrip_leg(wl, world, min(args.steps, 10))
+
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         cpu = cpu_baseline(wl, args.cpu_seconds)
@@ -583,6 +620,8 @@ def main():
                          "valu": valu_roofline(pmc, avg_kernel_s)},
             "cpu_baseline": cpu,
         }
+        if rtl is not None:
+            line["seal_open_verify"] = rtl
         if sg is not None:
             line["scatter_gather"] = sg
         print(json.dumps(line), flush=True)

@@ -24,7 +24,7 @@ for cfg in e2e4k engine beforenm; do
 done
 for cfg in 4k zipf open4k 100b; do
   echo "== rocprofv3 kernel trace $cfg"
-  timeout -k 10 300 rocprofv3 --kernel-trace --stats -T --output-format csv -d gpurun_out/prof_$cfg -o run -- python3 bench.py --steps 10 --warmup 2 --no-cpu-baseline --config $cfg > gpurun_out/prof_$cfg.log 2>&1 || { tail gpurun_out/prof_$cfg.log; exit 6; }
+  timeout -k 10 300 rocprofv3 --kernel-trace --stats -T --output-format csv -d gpurun_out/prof_$cfg -o run -- python3 bench.py --steps 10 --warmup 2 --no-cpu-baseline --no-roundtrip --config $cfg > gpurun_out/prof_$cfg.log 2>&1 || { tail gpurun_out/prof_$cfg.log; exit 6; }
 done
 bash tools/gpu_traffic.sh 4k 100b zipf open4k || exit 7
 bash tools/gpu_valu.sh 4k 100b zipf open4k || exit 8

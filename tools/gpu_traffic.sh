@@ -7,7 +7,7 @@ export TMPDIR=/tmp
 for cfg in "$@"; do
   for pmc in FETCH_SIZE WRITE_SIZE; do
     echo "== $cfg $pmc"
-    timeout -k 10 240 rocprofv3 --pmc $pmc --output-format csv -d gpurun_out/traffic_${cfg}_$pmc -o run --kernel-include-regex "k_seal|k_open" -- python3 bench.py --steps 3 --warmup 1 --ramp-ms 0 --no-cpu-baseline --config $cfg > gpurun_out/traffic_${cfg}_$pmc.log 2>&1 || { tail -5 gpurun_out/traffic_${cfg}_$pmc.log; exit 6; }
+    timeout -k 10 240 rocprofv3 --pmc $pmc --output-format csv -d gpurun_out/traffic_${cfg}_$pmc -o run --kernel-include-regex "k_seal|k_open" -- python3 bench.py --steps 3 --warmup 1 --ramp-ms 0 --no-cpu-baseline --no-roundtrip --config $cfg > gpurun_out/traffic_${cfg}_$pmc.log 2>&1 || { tail -5 gpurun_out/traffic_${cfg}_$pmc.log; exit 6; }
   done
 done
 python3 tools/traffic_update.py gpurun_out "$@"

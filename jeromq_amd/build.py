@@ -11,7 +11,7 @@ HERE = os.path.dirname(os.path.abspath(__file__))
 CSRC = os.path.join(HERE, "csrc")
 LIB = os.environ.get("CZ_LIB_OUT", os.path.join(HERE, "libcurvezmq_mi355x.so"))
 SOURCES = ["cz_kernels.hip", "cz_x25519.hip", "cz_host.cpp", "cz_mechanism.cpp", "cz_wire.cpp", "cz_engine.cpp", "cz_handshake.cpp"]
-HEADERS = ["cz_device.h", "cz_internal.h", os.path.join("..", "..", "include", "curvezmq_mi355x.h")]
+HEADERS = ["cz_device.h", "cz_internal.h", "cz_salsa_lazy.h", os.path.join("..", "..", "include", "curvezmq_mi355x.h")]
 ARCH = os.environ.get("CZ_OFFLOAD_ARCH", "gfx950")
 
 

@@ -75,6 +75,7 @@ constexpr int BLOCK = 256;              // threads per workgroup (4 waves)
 #endif
 constexpr int WAVES = BLOCK / 64;
 constexpr u32 LINE_LDS_BYTES = 64 * 128; // EmitLines: one 128-byte line per frame
+constexpr u32 HOLD_LDS_BYTES = 64 * 64;  // EmitLines (seal): block 1 of every frame, until tag()
 constexpr u32 REGION_MAX = 16384;       // EmitRegion: 64 slots per wave
 
 struct V4 {
@@ -112,10 +113,23 @@ __device__ __forceinline__ u32 ld32(const uint8_t *__restrict__ p)
         return (u32)p[0] | ((u32)p[1] << 8) | ((u32)p[2] << 16) | ((u32)p[3] << 24);
 }
 
+// Diagnostic builds only (tools/gpu_clock_ab.sh; never the shipped library, and their output
+// is wrong by construction): CZ_DIAG_NOLOAD makes full-chunk payload loads return address bits,
+// CZ_DIAG_NOSTORE drops EmitLines' line stores (kept for one impossible value), so the clock
+// and time of the 4k seal can be measured without its HBM reads or writes; CZ_DIAG_NOTAG writes
+// line 0 whole in the flush and drops the late 16-byte tag store; CZ_DIAG_L2STORE sends every
+// line store of a wave to the same 8 KiB (L2-resident, no HBM writes).
+
 // Unguarded full-chunk load (caller proved all 16 bytes valid).
 template <bool AL>
 __device__ __forceinline__ V4 ld16f(const uint8_t *__restrict__ p)
 {
+#ifdef CZ_DIAG_NOLOAD
+    if constexpr (AL) {
+        const u32 a = (u32)(uintptr_t)p;
+        return V4{a, a ^ 0x9e3779b9u, a + 0x7f4a7c15u, a ^ 0x85ebca6bu};
+    }
+#endif
     if constexpr (AL) {
         uint4 v = *reinterpret_cast<const uint4 *>(p);
         return V4{v.x, v.y, v.z, v.w};
@@ -231,21 +245,39 @@ struct EmitLines {
     uint8_t *mine;     // this lane's slot
     u64 stride;
     u32 lane, total, last_q;
-    bool tag_slot;     // seal: leave bytes 16..31 of line 0 to tag()
+    bool tag_slot;     // seal: line 0 (header, nonce, tag, first 96 ciphertext bytes) leaves whole in tag()
+    uint4 *hold;       // seal: this wave's 64 x 64 bytes, block 1 of every frame
+    u32 head[12];      // seal: block 0's words 0..3 and 8..15
+    u32 tagw[4];       // seal: the tag, staged with line 0 by close()
 
-    __device__ __forceinline__ void flush(u32 line)
+    __device__ __forceinline__ void flush(u32 line, bool whole = false)
     {
         const u32 c = lane & 7u;
         const u32 r = lane >> 3;
+#ifdef CZ_DIAG_L2STORE
+        uint8_t *p = wbase + 128u * r + 16u * c;  // every line of the wave onto its first 8 KiB
+        const u64 step = 1024u;
+#else
         uint8_t *p = wbase + (u64)r * stride + 128ull * line + 16u * c;
         const u64 step = 8ull * stride;
-        const bool skip = tag_slot && line == 0 && c == 1;
+#endif
+#ifdef CZ_DIAG_NOTAG
+        const bool skip = false;
+#else
+        // seal: line 0 leaves whole from close(), one full 128-byte line written once, not a
+        // 112-byte line and a late 16-byte tag (partial lines cost L2 fills)
+        const bool skip = tag_slot && line == 0 && !whole;
+#endif
         asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // the other lanes' ds_writes of this line
 #pragma unroll
         for (u32 j = 0; j < 8; j++) {
             const u32 F = 8u * j + r;
             uint4 v = lds[F * 8u + (c ^ (F & 7u))];
+#ifdef CZ_DIAG_NOSTORE
+            if (!skip && v.x == 0x13579bdfu && v.w == 0x2468ace0u)
+#else
             if (!skip)
+#endif
                 *reinterpret_cast<uint4 *>(p) = v;
             p += step;
         }
@@ -264,6 +296,19 @@ struct EmitLines {
     // copies merging masked and unmasked chunks) between the producer and the LDS writes
     __device__ __forceinline__ void emit_full(u32 q, const u32 D[16])
     {
+        if (tag_slot && q == 0u) {
+#pragma unroll
+            for (int k = 0; k < 4; k++)
+                head[k] = D[k];
+#pragma unroll
+            for (int k = 0; k < 8; k++)
+                head[4 + k] = D[8 + k];
+        }
+        if (tag_slot && q == 1u) {
+#pragma unroll
+            for (u32 c = 0; c < 4; c++)
+                hold[lane * 4u + c] = make_uint4(D[4 * c], D[4 * c + 1], D[4 * c + 2], D[4 * c + 3]);
+        }
         const u32 h = q & 1u;
         const u32 sw = lane & 7u;
 #pragma unroll
@@ -275,7 +320,34 @@ struct EmitLines {
     }
     __device__ __forceinline__ void tag(const u32 t[4])
     {
-        *reinterpret_cast<uint4 *>(mine + 16) = make_uint4(t[0], t[1], t[2], t[3]);
+#ifdef CZ_DIAG_NOTAG
+        if (t[0] == 0x13579bdfu && t[3] == 0x2468ace0u)
+            *reinterpret_cast<uint4 *>(mine + 16) = make_uint4(t[0], t[1], t[2], t[3]);
+#else
+#pragma unroll
+        for (int k = 0; k < 4; k++)
+            tagw[k] = t[k];
+#endif
+    }
+    // seal, converged, after the last line's flush: line 0 = block 0 (header, nonce, tag,
+    // 32 ciphertext bytes) + block 1 (held in LDS; zero if the frame has one block), staged
+    // and written with the same full-line stores as every other line
+    __device__ __forceinline__ void line0()
+    {
+        const u32 sw = lane & 7u;
+        const bool one = last_q == 0u;
+        uint4 b1[4];
+#pragma unroll
+        for (u32 c = 0; c < 4; c++)
+            b1[c] = one ? make_uint4(0u, 0u, 0u, 0u) : hold[lane * 4u + c];
+        lds[lane * 8u + (0u ^ sw)] = make_uint4(head[0], head[1], head[2], head[3]);
+        lds[lane * 8u + (1u ^ sw)] = make_uint4(tagw[0], tagw[1], tagw[2], tagw[3]);
+        lds[lane * 8u + (2u ^ sw)] = make_uint4(head[4], head[5], head[6], head[7]);
+        lds[lane * 8u + (3u ^ sw)] = make_uint4(head[8], head[9], head[10], head[11]);
+#pragma unroll
+        for (u32 c = 0; c < 4; c++)
+            lds[lane * 8u + ((4u + c) ^ sw)] = b1[c];
+        flush(0, true);
     }
     __device__ __forceinline__ void finish()
     {
@@ -287,10 +359,14 @@ struct EmitLines {
             flush(last_q >> 1);
         }
     }
-    // converged: flush the last line, then zero rejected frames' slots
+    // converged: flush the last line (and the seal's line 0), then zero rejected frames' slots
     __device__ __forceinline__ void close(bool bad)
     {
         finish();
+#ifndef CZ_DIAG_NOTAG
+        if (tag_slot)
+            line0();
+#endif
         if (bad)
             poison();
     }
@@ -1349,7 +1425,8 @@ __global__ __launch_bounds__(BLOCK) CZ_OCC void k_seal_uniform(const uint8_t *__
         const u32 lane = threadIdx.x & 63u;
         if constexpr (ST == ST_LINES) {
             EmitLines em{smem + (threadIdx.x >> 6) * (LINE_LDS_BYTES / 16), out + (uint64_t)wave_first * out_stride,
-                         dst, out_stride, lane, mlen, 0u, true};
+                         dst, out_stride, lane, mlen, 0u, true,
+                         smem + (WAVES * LINE_LDS_BYTES + (threadIdx.x >> 6) * HOLD_LDS_BYTES) / 16};
             if (un0)
                 seal_frame<MODE_ZMQ, true, EmitLines, PAIR, true>(src, len, fl, counter0 + i, key, em);
             else
@@ -1890,7 +1967,8 @@ hipError_t czk_seal_uniform(const void *in, uint64_t in_stride, void *out, uint6
     hipLaunchKernelGGL((k_seal_uniform<ST, PR>), grid, dim3(BLOCK), (LDS), s, (const uint8_t *)in, in_stride,   \
                        (uint8_t *)out, out_stride, count, len, (const uint8_t *)subkey, counter0, flags8, g_un0)
     const int st = pick_staging(out_stride, len + 33u, al);
-    const unsigned lds = st == ST_LINES ? WAVES * LINE_LDS_BYTES : (st == ST_REGION ? (unsigned)(WAVES * 64 * out_stride) : 0u);
+    const unsigned lds = st == ST_LINES ? WAVES * (LINE_LDS_BYTES + HOLD_LDS_BYTES)
+                                        : (st == ST_REGION ? (unsigned)(WAVES * 64 * out_stride) : 0u);
     // whole-line input pays for large frames (A/B: 4 KiB seal 2.34 vs 2.51 ms) but
     // not for the small frames of the region stager (100 B: 0.119 vs 0.114 ms)
     if (g_pair && st != ST_REGION) {

@@ -278,7 +278,15 @@ struct EmitLines {
 #else
             if (!skip)
 #endif
+#ifdef CZ_DIAG_STORE_POLICY  // cache-policy bits on the line stores, e.g. -DCZ_DIAG_STORE_POLICY='"sc1"'
+            {
+                typedef unsigned v4u __attribute__((ext_vector_type(4)));
+                const v4u d = {v.x, v.y, v.z, v.w};
+                asm volatile("global_store_dwordx4 %0, %1, off " CZ_DIAG_STORE_POLICY ::"v"(p), "v"(d) : "memory");
+            }
+#else
                 *reinterpret_cast<uint4 *>(p) = v;
+#endif
             p += step;
         }
     }

@@ -254,6 +254,8 @@ UNIFORM_CASES = [
     (100, 112, 256, 640),            # REGION with 256-byte slots
     (1000, 1008, 1152, 777),         # LINES, mid-size
     (223, 224, 256, 300),            # body 256 B exactly: LINES
+    (300, 304, 384, 200),            # LINES, 6 blocks, 13-byte last block, 3 lines
+    (4000, 4000, 4096, 130),         # LINES, last line 33 bytes short of the slot
     (0, 16, 48, 200),                # empty payloads: REGION
     (31, 32, 128, 130),              # body = 64 B (block-0 only): REGION
 ]

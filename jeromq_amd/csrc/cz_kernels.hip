@@ -68,6 +68,11 @@ constexpr int BLOCK = 256;              // threads per workgroup (4 waves)
 #else
 #define CZ_OCC
 #endif
+// k_seal_segments_lines: 3 waves per SIMD unless CZ_SEG_LINES_WAVES_PER_EU says otherwise
+#ifndef CZ_SEG_LINES_WAVES_PER_EU
+#define CZ_SEG_LINES_WAVES_PER_EU 3
+#endif
+#define CZ_SEG_LINES_OCC __attribute__((amdgpu_waves_per_eu(CZ_SEG_LINES_WAVES_PER_EU, CZ_SEG_LINES_WAVES_PER_EU)))
 #ifdef CZ_SEG_WAVES_PER_EU
 #define CZ_SEG_OCC __attribute__((amdgpu_waves_per_eu(CZ_SEG_WAVES_PER_EU, CZ_SEG_WAVES_PER_EU)))
 #else
@@ -1068,7 +1073,7 @@ __device__ __forceinline__ u32 seal_seg_bytes(u32 mlen, u32 b0, u32 bend)
 // most lines twice (2.6x the payload on the Zipf batch).
 template <bool AL, class EM, bool PAIR = false>
 __device__ void seal_segment(const uint8_t *__restrict__ in, u32 n, u32 flags, u64 counter, const u32 key[8], u32 b0,
-                             u32 b1, u32 *__restrict__ rec, EM &em)
+                             u32 b1, u32 *__restrict__ rec, EM &em, u32 nrun = 0)
 {
     const u32 mlen = n + 33u;
     const u32 nblk = (mlen + 63u) >> 6;
@@ -1084,8 +1089,10 @@ __device__ void seal_segment(const uint8_t *__restrict__ in, u32 n, u32 flags, u
     poly_init(P, x[0], x[1], x[2], x[3], x[4], x[5], x[6], x[7]);
     u32 mpoly = 0;
 
-    // box block blk from its 17-dword window W = P[16blk-9 .. 16blk+7] (P[-1] = flags << 24)
-    auto block = [&](u32 blk, const u32 *W) {
+    // box block blk from its 17-dword window W = P[16blk-9 .. 16blk+7] (P[-1] = flags << 24);
+    // own = false: a block past this lane's segment, run only to keep the wave in step
+    // (PAIR with nrun > nch): not absorbed, and its stores are clipped by the emitter
+    auto block = [&](u32 blk, const u32 *W, bool own = true) {
         salsa20_block(x, key, n0, n1, blk, 0u);
 #pragma unroll
         for (int k = 0; k < 16; k++)
@@ -1094,7 +1101,8 @@ __device__ void seal_segment(const uint8_t *__restrict__ in, u32 n, u32 flags, u
             C[0] = HDR0; C[1] = HDR1; C[2] = n0; C[3] = n1;
             C[4] = C[5] = C[6] = C[7] = 0u;  // tag slot
         }
-        if (blk != 0 && blk < nfull) {
+        if (!own) {
+        } else if (blk != 0 && blk < nfull) {
             poly_block(P, C[0], C[1], C[2], C[3], 1u);
             poly_block(P, C[4], C[5], C[6], C[7], 1u);
             poly_block(P, C[8], C[9], C[10], C[11], 1u);
@@ -1130,7 +1138,9 @@ __device__ void seal_segment(const uint8_t *__restrict__ in, u32 n, u32 flags, u
             cy[0] = a.w; cy[1] = b.x; cy[2] = b.y; cy[3] = b.z; cy[4] = b.w;
             cy[5] = c.x; cy[6] = c.y; cy[7] = c.z; cy[8] = c.w;
         }
-        for (u32 q = 0; q < nch; q += 2u) {
+        // nrun (cooperative emitters): the wave's longest segment; shorter ones run along
+        const u32 run = nrun > nch ? nrun : nch;
+        for (u32 q = 0; q < run; q += 2u) {
             const u32 blk = b0 + q;
             const uint8_t *src = in + 64u * blk;
             const u64 o = 64ull * blk;
@@ -1155,10 +1165,10 @@ __device__ void seal_segment(const uint8_t *__restrict__ in, u32 n, u32 flags, u
 #pragma unroll
             for (int k = 0; k < 8; k++)
                 W[9 + k] = L[k];
-            block(blk, W);
+            block(blk, W, q < nch);
             em.emit(q, C);
-            if (q + 1u < nch) {
-                block(blk + 1u, L + 7);
+            if (q + 1u < run) {
+                block(blk + 1u, L + 7, q + 1u < nch);
                 em.emit(q + 1u, C);
             }
 #pragma unroll
@@ -1596,6 +1606,22 @@ constexpr int SEGMODE_PAIR = 2;   // whole-line input loads (seal)
 
 // A wave takes the line emitter when all 64 lanes hold segments with the same
 // chunk count and 16-byte aligned input/output; otherwise each lane stores directly.
+// Seal, whole-line loads: a full wave of aligned segments may mix chunk counts; shorter
+// segments run along to the wave's longest (wave_max) with their extra blocks discarded.
+__device__ __forceinline__ bool wave_lines_ragged_ok(bool full_wave, bool al)
+{
+    return full_wave && __builtin_amdgcn_ballot_w64(!al) == 0;
+}
+__device__ __forceinline__ u32 wave_max(u32 v)
+{
+#pragma unroll
+    for (int o = 32; o >= 1; o >>= 1) {
+        const u32 w = (u32)__shfl_xor((int)v, o);
+        v = w > v ? w : v;
+    }
+    return v;
+}
+
 __device__ __forceinline__ bool wave_lines_ok(bool full_wave, u32 nchunks, bool al)
 {
     if (!full_wave)
@@ -1603,13 +1629,23 @@ __device__ __forceinline__ bool wave_lines_ok(bool full_wave, u32 nchunks, bool 
     return wave_uniform(nchunks) && __builtin_amdgcn_ballot_w64(!al) == 0;
 }
 
-__global__ __launch_bounds__(BLOCK) CZ_SEG_OCC void k_seal_segments(const cz_frame_desc *__restrict__ desc,
-                                                          const cz_segment *__restrict__ segs, uint32_t nseg,
-                                                          const uint8_t *__restrict__ in, uint8_t *__restrict__ out,
-                                                          const uint8_t *__restrict__ subkeys,
-                                                          u32 *__restrict__ work, int mode)
+constexpr int SEGMODE_REST = 4;   // k_seal_segments: only the waves k_seal_segments_lines leaves
+
+// Segment kernels.  With line staging and whole-line loads enabled the launcher runs two
+// kernels over the same segment list: k_seal_segments_lines takes every full wave of aligned
+// segments (wave_lines_ragged_ok) and is built for 3 waves per SIMD (168 VGPRs; its single
+// path fits them, while the general kernel needs ~190 and runs 2); k_seal_segments with
+// SEGMODE_REST then takes exactly the other waves (same predicate, inverted: the partial last
+// wave and unaligned buffers).  Without those modes k_seal_segments alone runs every wave.
+enum { SEGPART_ALL = 0, SEGPART_LINES = 1, SEGPART_REST = 2 };
+
+template <int PART>
+__device__ __forceinline__ void seal_segments_body(const cz_frame_desc *__restrict__ desc,
+                                                   const cz_segment *__restrict__ segs, uint32_t nseg,
+                                                   const uint8_t *__restrict__ in, uint8_t *__restrict__ out,
+                                                   const uint8_t *__restrict__ subkeys, u32 *__restrict__ work,
+                                                   int mode, uint4 *smem)
 {
-    extern __shared__ uint4 smem[];
     const uint32_t t = blockIdx.x * BLOCK + threadIdx.x;
     const uint32_t wave_first = t & ~63u;
     if (wave_first >= nseg)
@@ -1618,8 +1654,6 @@ __global__ __launch_bounds__(BLOCK) CZ_SEG_OCC void k_seal_segments(const cz_fra
     const bool live = t < nseg;
     const cz_segment sg = segs[live ? t : wave_first];
     const cz_frame_desc d = desc[sg.frame];
-    u32 key[8];
-    load_key(subkeys + 32ull * d.key_idx, key);
     u32 *rec = sg.part == 0xffffffffu ? nullptr : work + 16ull * sg.part;
     const uint8_t *src = in + d.in_off;
     uint8_t *dst = out + d.out_off + 64ull * sg.first_block;
@@ -1629,31 +1663,70 @@ __global__ __launch_bounds__(BLOCK) CZ_SEG_OCC void k_seal_segments(const cz_fra
     const u32 nch = (b1 < nblk ? b1 : nblk) - sg.first_block;
     const u32 total = seal_seg_bytes(mlen, sg.first_block, b1 < nblk ? b1 : nblk);
     const bool al = aligned16(src, dst);
-    if (allow_lines && wave_lines_ok(wave_first + 64u <= nseg, nch, al)) {
-        const u32 lane = threadIdx.x & 63u;
-        uint8_t *wl = reinterpret_cast<uint8_t *>(smem) + (threadIdx.x >> 6) * SEG_LDS_BYTES;
-        EmitSegLines em{reinterpret_cast<uint4 *>(wl), dst, lane, total, 0u, 0u};
-        em.init(sg.first_block == 0);
-        if (pair)
-            seal_segment<true, EmitSegLines, true>(src, d.len, d.flags & 0xffu, d.counter, key, sg.first_block, b1,
-                                                   rec, em);
-        else
-            seal_segment<true>(src, d.len, d.flags & 0xffu, d.counter, key, sg.first_block, b1, rec, em);
-        return;
+    const bool full_wave = wave_first + 64u <= nseg;
+    const bool lines = allow_lines && (pair ? wave_lines_ragged_ok(full_wave, al) : wave_lines_ok(full_wave, nch, al));
+    if constexpr (PART == SEGPART_LINES) {
+        if (!lines)
+            return;
     }
-    if (!live)
-        return;
-    if (al) {
-        EmitDirect<true> em{dst, total};
-        if (pair)
-            seal_segment<true, EmitDirect<true>, true>(src, d.len, d.flags & 0xffu, d.counter, key, sg.first_block,
-                                                       b1, rec, em);
-        else
-            seal_segment<true>(src, d.len, d.flags & 0xffu, d.counter, key, sg.first_block, b1, rec, em);
-    } else {
-        EmitDirect<false> em{dst, total};
-        seal_segment<false>(src, d.len, d.flags & 0xffu, d.counter, key, sg.first_block, b1, rec, em);
+    if constexpr (PART == SEGPART_REST) {
+        if (lines)
+            return;
     }
+    u32 key[8];
+    load_key(subkeys + 32ull * d.key_idx, key);
+    if constexpr (PART != SEGPART_REST) {
+        if (lines) {
+            const u32 lane = threadIdx.x & 63u;
+            uint8_t *wl = reinterpret_cast<uint8_t *>(smem) + (threadIdx.x >> 6) * SEG_LDS_BYTES;
+            EmitSegLines em{reinterpret_cast<uint4 *>(wl), dst, lane, total, 0u, 0u};
+            em.init(sg.first_block == 0);
+            if (PART == SEGPART_LINES || pair)
+                seal_segment<true, EmitSegLines, true>(src, d.len, d.flags & 0xffu, d.counter, key, sg.first_block,
+                                                       b1, rec, em, wave_max(nch));
+            else
+                seal_segment<true>(src, d.len, d.flags & 0xffu, d.counter, key, sg.first_block, b1, rec, em);
+            return;
+        }
+    }
+    if constexpr (PART != SEGPART_LINES) {
+        if (!live)
+            return;
+        if (al) {
+            EmitDirect<true> em{dst, total};
+            if (pair)
+                seal_segment<true, EmitDirect<true>, true>(src, d.len, d.flags & 0xffu, d.counter, key,
+                                                           sg.first_block, b1, rec, em);
+            else
+                seal_segment<true>(src, d.len, d.flags & 0xffu, d.counter, key, sg.first_block, b1, rec, em);
+        } else {
+            EmitDirect<false> em{dst, total};
+            seal_segment<false>(src, d.len, d.flags & 0xffu, d.counter, key, sg.first_block, b1, rec, em);
+        }
+    }
+}
+
+__global__ __launch_bounds__(BLOCK) CZ_SEG_OCC void k_seal_segments(const cz_frame_desc *__restrict__ desc,
+                                                          const cz_segment *__restrict__ segs, uint32_t nseg,
+                                                          const uint8_t *__restrict__ in, uint8_t *__restrict__ out,
+                                                          const uint8_t *__restrict__ subkeys,
+                                                          u32 *__restrict__ work, int mode)
+{
+    extern __shared__ uint4 smem[];
+    if (mode & SEGMODE_REST)
+        seal_segments_body<SEGPART_REST>(desc, segs, nseg, in, out, subkeys, work, mode, smem);
+    else
+        seal_segments_body<SEGPART_ALL>(desc, segs, nseg, in, out, subkeys, work, mode, smem);
+}
+
+// mode must hold SEGMODE_LINES | SEGMODE_PAIR
+__global__ __launch_bounds__(BLOCK) CZ_SEG_LINES_OCC void k_seal_segments_lines(
+    const cz_frame_desc *__restrict__ desc, const cz_segment *__restrict__ segs, uint32_t nseg,
+    const uint8_t *__restrict__ in, uint8_t *__restrict__ out, const uint8_t *__restrict__ subkeys,
+    u32 *__restrict__ work, int mode)
+{
+    extern __shared__ uint4 smem[];
+    seal_segments_body<SEGPART_LINES>(desc, segs, nseg, in, out, subkeys, work, mode, smem);
 }
 
 __global__ __launch_bounds__(BLOCK) void k_seal_combine(const cz_frame_desc *__restrict__ desc,
@@ -2064,10 +2137,22 @@ hipError_t czk_subkeys(const void *precom, void *out, uint32_t nkeys, const uint
 hipError_t czk_seal_segments(const cz_frame_desc *desc, const cz_segment *segs, uint32_t nseg, const cz_combine *comb,
                              uint32_t ncomb, const void *in, void *out, const void *subkeys, void *work, hipStream_t s)
 {
-    if (nseg)
-        hipLaunchKernelGGL(k_seal_segments, dim3((nseg + BLOCK - 1) / BLOCK), dim3(BLOCK), WAVES * SEG_LDS_BYTES, s,
-                           desc, segs, nseg, (const uint8_t *)in, (uint8_t *)out, (const uint8_t *)subkeys,
-                           (u32 *)work, (g_seglines ? SEGMODE_LINES : 0) | (g_pair ? SEGMODE_PAIR : 0));
+    const dim3 grid((nseg + BLOCK - 1) / BLOCK);
+#ifdef CZ_SEG_SINGLE_KERNEL  // A/B: one k_seal_segments launch for every wave
+    if (false) {
+#else
+    if (nseg && g_seglines && g_pair) {
+#endif
+        const int mode = SEGMODE_LINES | SEGMODE_PAIR;
+        hipLaunchKernelGGL(k_seal_segments_lines, grid, dim3(BLOCK), WAVES * SEG_LDS_BYTES, s, desc, segs, nseg,
+                           (const uint8_t *)in, (uint8_t *)out, (const uint8_t *)subkeys, (u32 *)work, mode);
+        hipLaunchKernelGGL(k_seal_segments, grid, dim3(BLOCK), 0, s, desc, segs, nseg, (const uint8_t *)in,
+                           (uint8_t *)out, (const uint8_t *)subkeys, (u32 *)work, mode | SEGMODE_REST);
+    } else if (nseg) {
+        hipLaunchKernelGGL(k_seal_segments, grid, dim3(BLOCK), WAVES * SEG_LDS_BYTES, s, desc, segs, nseg,
+                           (const uint8_t *)in, (uint8_t *)out, (const uint8_t *)subkeys, (u32 *)work,
+                           (g_seglines ? SEGMODE_LINES : 0) | (g_pair ? SEGMODE_PAIR : 0));
+    }
     if (ncomb)
         hipLaunchKernelGGL(k_seal_combine, dim3((ncomb + BLOCK - 1) / BLOCK), dim3(BLOCK), 0, s, desc, comb, ncomb,
                            (uint8_t *)out, (const u32 *)work);

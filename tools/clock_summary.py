@@ -11,7 +11,7 @@ import sys
 
 root, tag = sys.argv[1], sys.argv[2]
 cfg = sys.argv[3] if len(sys.argv) > 3 else "4k"
-KERNEL = {"4k": "k_seal_uniform", "100b": "k_seal_uniform", "open4k": "k_open_uniform", "zipf": "k_seal_segments"}[cfg]
+KERNEL = {"4k": "k_seal_uniform", "100b": "k_seal_uniform", "open4k": "k_open_uniform", "zipf": "k_seal_segments_lines"}[cfg]
 line = json.loads(open(os.path.join(root, f"clk_{tag}.log")).read().strip().splitlines()[-1])
 rows = collections.defaultdict(dict)
 for f in glob.glob(os.path.join(root, f"clkpmc_{tag}", "**", "*counter_collection.csv"), recursive=True):

@@ -8,7 +8,7 @@ import statistics
 import sys
 
 root, cfg = sys.argv[1], sys.argv[2]
-KERNEL = {"4k": "k_seal_uniform", "100b": "k_seal_uniform", "open4k": "k_open_uniform", "zipf": "k_seal_segments"}[cfg]
+KERNEL = {"4k": "k_seal_uniform", "100b": "k_seal_uniform", "open4k": "k_open_uniform", "zipf": "k_seal_segments_lines"}[cfg]
 vals = collections.defaultdict(list)
 for p in (1, 2):
     rows = collections.defaultdict(dict)

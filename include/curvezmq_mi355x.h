@@ -43,6 +43,9 @@ extern "C" {
 #define CZ_MACBYTES 16
 /* MESSAGE body = "\x07MESSAGE"(8) + nonce8 + tag16 + flags(1) + payload */
 #define CZ_MESSAGE_OVERHEAD 33
+/* largest MESSAGE payload: the body (payload + 33) must fit a Java int, as every Msg size does
+ * (Msg.java size(): int); encode / encode_batch / cz_engine_send return CZ_EMSGSIZE beyond it */
+#define CZ_MESSAGE_MAX (0x7fffffff - CZ_MESSAGE_OVERHEAD)
 
 /* Msg flags carried in the encrypted flags byte (Msg.java:96-100, CurveClientMechanism.java:131-137) */
 #define CZ_MSG_MORE 0x01
@@ -67,6 +70,7 @@ extern "C" {
 #define CZ_ENOMEM (-12)
 #define CZ_EPROTO (-71)
 #define CZ_EMSGSIZE (-90)
+#define CZ_EAGAIN (-11)
 
 /* cz_frame_desc.flags bits (seal: low byte = the MESSAGE flags byte) */
 #define CZ_DESC_CHECK_NONCE 0x100 /* open: enforce nonce > floor (counter or prev frame's nonce) */
@@ -235,6 +239,14 @@ uint64_t cz_mech_peer_nonce(const cz_mech *m);
 #define CZ_ZMTP_MALFORMED_COMMAND_MESSAGE 0x10000012
 #define CZ_ZMTP_INVALID_SEQUENCE 0x10000002
 #define CZ_ZMTP_CRYPTOGRAPHIC 0x11000001
+#define CZ_ZMTP_UNSPECIFIED 0x10000000
+#define CZ_ZMTP_KEY_EXCHANGE 0x10000003
+#define CZ_ZMTP_MALFORMED_COMMAND_HELLO 0x10000013
+#define CZ_ZMTP_MALFORMED_COMMAND_INITIATE 0x10000014
+#define CZ_ZMTP_MALFORMED_COMMAND_ERROR 0x10000015
+#define CZ_ZMTP_MALFORMED_COMMAND_READY 0x10000016
+#define CZ_ZAP_MALFORMED_REPLY 0x20000001
+#define CZ_ZAP_INVALID_STATUS_CODE 0x20000004
 
 /* ---- 7. ZMTP v2 framing (zmq/io/coder/v2/V2Encoder.java, V2Decoder.java) ----------------
  * Wire frame = flags byte (MORE 1, LARGE 2, COMMAND 4: V1Protocol/V2Protocol) + size
@@ -328,6 +340,53 @@ int cz_box_open(uint8_t *m, const uint8_t *c, uint64_t clen, const uint8_t n[24]
  * k[i] = beforenm(pk[i], sk[i]) = HSalsa20(X25519(sk[i], pk[i]), 0^16). */
 int cz_x25519_batch(const void *d_scalars, const void *d_points, void *d_out, uint32_t count, void *stream);
 int cz_beforenm_batch(const void *d_pk, const void *d_sk, void *d_k, uint32_t count, void *stream);
+
+/* ---- 10. CURVE handshake: HELLO / WELCOME / INITIATE / READY (+ ERROR) -----------------------------
+ * The state machines of CurveClientMechanism (:80-124, :246-429) and CurveServerMechanism
+ * (:77-126, :227-517) with every box / open / secretbox / beforenm / X25519 on the GPU (section 9).
+ * A handshake object is created in the reference constructor's state (fresh short-term key pair,
+ * cnNonce = cnPeerNonce = 1); the caller moves ZMTP command bodies between the peers:
+ *   cz_hs_next_command   = Mechanism.nextHandshakeCommand: CZ_OK with a command to send,
+ *                          CZ_EAGAIN when there is nothing to send in this state;
+ *   cz_hs_process_command = Mechanism.processHandshakeCommand: CZ_OK, or CZ_EPROTO with
+ *                          cz_hs_event() = the ZMQ_PROTOCOL_ERROR_* event the reference raises,
+ *                          CZ_EINVAL for an incompatible peer Socket-Type (parseMetadata);
+ *   cz_hs_status         = Mechanism.status: CZ_HS_HANDSHAKING / READY / ERROR.
+ * Once READY, cz_hs_session yields cnPrecom and the nonce counters that cz_mech_create /
+ * cz_engine_add_conn take; cz_hs_mechanism / cz_engine_add_session do both steps.
+ * socket_type: ZMQ_PAIR = 0 ... ZMQ_GATHER = 20 (zmq/ZMQ.java:50-70); the Socket-Type property and,
+ * for REQ / DEALER / ROUTER, the Identity property are sent in INITIATE / READY.
+ * ephemeral_secret / entropy (tests only, NULL in production): a fixed short-term secret and the
+ * bytes the reference's Curve.random() draws return, in order (client: the 16-byte vouch nonce;
+ * server: cookie nonce 16, cookie key 32, WELCOME nonce 16).  ZAP (out of scope): with
+ * cz_hs_set_zap(hs, 1) the server waits after INITIATE for cz_hs_zap_reply(hs, "200" | "4xx" ...). */
+typedef struct cz_hs cz_hs;
+#define CZ_HS_HANDSHAKING 0
+#define CZ_HS_READY 1
+#define CZ_HS_ERROR 2
+int cz_hs_create(cz_hs **hs, int as_server, const uint8_t public_key[32], const uint8_t secret_key[32],
+                 const uint8_t server_key[32], int socket_type, const uint8_t *identity, uint32_t identity_len,
+                 const uint8_t *ephemeral_secret, const uint8_t *entropy, uint32_t entropy_len);
+void cz_hs_destroy(cz_hs *hs);
+int cz_hs_next_command(cz_hs *hs, uint8_t *out, uint32_t cap, uint32_t *len);
+int cz_hs_process_command(cz_hs *hs, const uint8_t *cmd, uint64_t size);
+int cz_hs_status(const cz_hs *hs);
+int cz_hs_event(const cz_hs *hs);
+/* client: the status code (300..500) of a well-formed ERROR from the server, else 0 */
+int cz_hs_error_status(const cz_hs *hs);
+int cz_hs_set_zap(cz_hs *hs, int on);
+int cz_hs_zap_reply(cz_hs *hs, const char *status_code);
+/* server, after INITIATE: the client's long-term public key C (what a ZAP request carries) */
+int cz_hs_client_key(const cz_hs *hs, uint8_t key[32]);
+int cz_hs_session(const cz_hs *hs, uint8_t precom[32], uint64_t *cn_nonce, uint64_t *cn_peer_nonce);
+/* a property of the peer's metadata (INITIATE / READY), e.g. "Socket-Type", "Identity" */
+int cz_hs_peer_property(const cz_hs *hs, const char *name, const uint8_t **value, uint32_t *len);
+cz_mech *cz_hs_mechanism(const cz_hs *hs, int device);
+int cz_engine_add_session(cz_engine *e, const cz_hs *hs);
+/* host only: Metadata.read + parseMetadata's Socket-Type check (CZ_OK / CZ_EPROTO / CZ_EINVAL), and the
+ * metadata block a socket of this type sends (returns its size; written when it fits in cap) */
+int cz_zmtp_metadata_check(const uint8_t *buf, uint64_t len, int socket_type);
+uint32_t cz_zmtp_metadata(int socket_type, const uint8_t *identity, uint32_t identity_len, uint8_t *out, uint32_t cap);
 
 /* ---- 6. misc -------------------------------------------------------------- */
 const char *cz_last_error(void);

@@ -17,6 +17,12 @@ CZ_EHIP = -5
 CZ_ENOMEM = -12
 CZ_EPROTO = -71
 CZ_EMSGSIZE = -90
+CZ_EAGAIN = -11
+CZ_MESSAGE_MAX = 0x7fffffff - 33
+
+CZ_HS_HANDSHAKING = 0
+CZ_HS_READY = 1
+CZ_HS_ERROR = 2
 
 CZ_STATUS_OK = 0
 CZ_STATUS_CRYPTO = 1
@@ -40,6 +46,14 @@ CZ_ZMTP_UNEXPECTED_COMMAND = 0x10000001
 CZ_ZMTP_MALFORMED_COMMAND_MESSAGE = 0x10000012
 CZ_ZMTP_INVALID_SEQUENCE = 0x10000002
 CZ_ZMTP_CRYPTOGRAPHIC = 0x11000001
+CZ_ZMTP_UNSPECIFIED = 0x10000000
+CZ_ZMTP_KEY_EXCHANGE = 0x10000003
+CZ_ZMTP_MALFORMED_COMMAND_HELLO = 0x10000013
+CZ_ZMTP_MALFORMED_COMMAND_INITIATE = 0x10000014
+CZ_ZMTP_MALFORMED_COMMAND_ERROR = 0x10000015
+CZ_ZMTP_MALFORMED_COMMAND_READY = 0x10000016
+CZ_ZAP_MALFORMED_REPLY = 0x20000001
+CZ_ZAP_INVALID_STATUS_CODE = 0x20000004
 
 
 class CzError(RuntimeError):
@@ -134,6 +148,22 @@ SIGNATURES = {
     "cz_box_open": (_I, [_VP, _VP, _U64, _VP, _VP, _VP]),
     "cz_x25519_batch": (_I, [_VP, _VP, _VP, _U32, _VP]),
     "cz_beforenm_batch": (_I, [_VP, _VP, _VP, _U32, _VP]),
+    "cz_hs_create": (_I, [ctypes.POINTER(_VP), _I, _VP, _VP, _VP, _I, _VP, _U32, _VP, _VP, _U32]),
+    "cz_hs_destroy": (None, [_VP]),
+    "cz_hs_next_command": (_I, [_VP, _VP, _U32, ctypes.POINTER(_U32)]),
+    "cz_hs_process_command": (_I, [_VP, _VP, _U64]),
+    "cz_hs_status": (_I, [_VP]),
+    "cz_hs_event": (_I, [_VP]),
+    "cz_hs_error_status": (_I, [_VP]),
+    "cz_hs_set_zap": (_I, [_VP, _I]),
+    "cz_hs_zap_reply": (_I, [_VP, ctypes.c_char_p]),
+    "cz_hs_client_key": (_I, [_VP, _VP]),
+    "cz_hs_session": (_I, [_VP, _VP, ctypes.POINTER(_U64), ctypes.POINTER(_U64)]),
+    "cz_hs_peer_property": (_I, [_VP, ctypes.c_char_p, ctypes.POINTER(_VP), ctypes.POINTER(_U32)]),
+    "cz_hs_mechanism": (_VP, [_VP, _I]),
+    "cz_engine_add_session": (_I, [_VP, _VP]),
+    "cz_zmtp_metadata_check": (_I, [_VP, _U64, _I]),
+    "cz_zmtp_metadata": (_U32, [_I, _VP, _U32, _VP, _U32]),
     "cz_last_error": (ctypes.c_char_p, []),
     "cz_version": (ctypes.c_char_p, []),
     "cz_device_ok": (_I, []),

@@ -10,7 +10,7 @@ import sys
 HERE = os.path.dirname(os.path.abspath(__file__))
 CSRC = os.path.join(HERE, "csrc")
 LIB = os.environ.get("CZ_LIB_OUT", os.path.join(HERE, "libcurvezmq_mi355x.so"))
-SOURCES = ["cz_kernels.hip", "cz_x25519.hip", "cz_host.cpp", "cz_mechanism.cpp", "cz_wire.cpp", "cz_engine.cpp", "cz_handshake.cpp"]
+SOURCES = ["cz_kernels.hip", "cz_x25519.hip", "cz_host.cpp", "cz_mechanism.cpp", "cz_wire.cpp", "cz_engine.cpp", "cz_handshake.cpp", "cz_curve_hs.cpp"]
 HEADERS = ["cz_device.h", "cz_internal.h", "cz_salsa_lazy.h", os.path.join("..", "..", "include", "curvezmq_mi355x.h")]
 ARCH = os.environ.get("CZ_OFFLOAD_ARCH", "gfx950")
 

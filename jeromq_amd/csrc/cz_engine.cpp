@@ -520,6 +520,8 @@ struct cz_engine {
                 const uint32_t i = p.first + k;
                 const uint32_t status = st[i] & 0xffu;
                 if (status != CZ_STATUS_OK) {
+                    if (status == CZ_STATUS_CRYPTO)  // the nonce passed the replay check: cnPeerNonce = nonce
+                        c.peer_nonce = nn[i];        // precedes openAfternm (CurveClientMechanism.java:193)
                     c.error = CZ_EPROTO;
                     c.event = event_for(status, c.server);
                     failed = true;
@@ -637,6 +639,8 @@ int cz_engine_send(cz_engine *e, int conn, const void *payload, uint32_t len, in
         return CZ_EINVAL;
     if (c->error)
         return fail(c->error, "cz_engine_send: connection %d has failed", conn);
+    if (len > (uint32_t)CZ_MESSAGE_MAX)
+        return fail(CZ_EMSGSIZE, "cz_engine_send: %u-byte payload exceeds CZ_MESSAGE_MAX", len);
     const uint8_t *base = (const uint8_t *)e->arena.ptr;
     const uint8_t *p = (const uint8_t *)payload;
     uint64_t off;

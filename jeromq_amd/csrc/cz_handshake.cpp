@@ -52,8 +52,13 @@ int hs_one(uint8_t out[32], const uint8_t scalar[32], const uint8_t *point, int 
     if ((e = hipMemcpyAsync(d, scalar, 32, hipMemcpyHostToDevice, t_hs.stream)) != hipSuccess ||
         (point && (e = hipMemcpyAsync(d + 32, point, 32, hipMemcpyHostToDevice, t_hs.stream)) != hipSuccess) ||
         (e = czk_x25519(d, point ? d + 32 : nullptr, d + 64, 1, beforenm, t_hs.stream)) != hipSuccess ||
-        (e = hipMemcpyAsync(out, d + 64, 32, hipMemcpyDeviceToHost, t_hs.stream)) != hipSuccess ||
-        (e = hipMemsetAsync(d, 0, 96, t_hs.stream)) != hipSuccess ||  // do not leave key material behind
+        (e = hipMemcpyAsync(out, d + 64, 32, hipMemcpyDeviceToHost, t_hs.stream)) != hipSuccess) {
+        // do not leave key material behind, on the error path either
+        (void)hipMemsetAsync(d, 0, 96, t_hs.stream);
+        (void)hipStreamSynchronize(t_hs.stream);
+        return hip_fail(e, "x25519");
+    }
+    if ((e = hipMemsetAsync(d, 0, 96, t_hs.stream)) != hipSuccess ||  // do not leave key material behind
         (e = hipStreamSynchronize(t_hs.stream)) != hipSuccess)
         return hip_fail(e, "x25519");
     return CZ_OK;

@@ -25,7 +25,6 @@ hipError_t czk_open_desc(const cz_frame_desc *, const uint32_t *, uint32_t, cons
 hipError_t czk_open_uniform(const void *, uint64_t, void *, uint64_t, uint32_t, uint32_t, const void *, uint64_t, int,
                             uint16_t *, hipStream_t);
 hipError_t czk_box_nacl(const void *, void *, uint32_t, const void *, uint64_t, int, int *, hipStream_t);
-hipError_t czk_subkeys(const void *, void *, uint32_t, const uint8_t *, hipStream_t);
 hipError_t czk_fill(void *, uint64_t, uint64_t, hipStream_t);
 int czk_tune(const char *, int);
 }
@@ -103,14 +102,16 @@ void HostBuf::release()
 }
 
 // ---- per-thread single-shot context ----------------------------------------
+// One message per call (the jnacl drop-ins).  Messages of more than a few blocks run through the
+// segment planner and kernels, so a 64 KiB box spreads over ~130 lanes instead of walking 1025
+// Salsa20 blocks on one lane (k_box_nacl keeps only mlen == 32, which has no MESSAGE form).
+// Everything the device needs -- key, descriptor, segment and combine lists, the message -- goes
+// over in ONE pinned H2D copy, and the result in one D2H copy.
 struct Single {
     bool ready = false;
     hipStream_t stream = nullptr;
-    DevBuf in, out, key, sub, rc;
-    ~Single()
-    {
-        // thread exit: best effort (the runtime may already be torn down at process exit)
-    }
+    DevBuf dev, rc;
+    HostBuf stage;
 };
 
 static thread_local Single t_single;
@@ -126,14 +127,28 @@ static int single_init()
     e = hipStreamCreateWithFlags(&t_single.stream, hipStreamNonBlocking);
     if (e != hipSuccess)
         return hip_fail(e, "hipStreamCreate");
-    if ((e = t_single.key.reserve(64)) != hipSuccess || (e = t_single.sub.reserve(64)) != hipSuccess ||
-        (e = t_single.rc.reserve(64)) != hipSuccess)
+    if ((e = t_single.rc.reserve(64)) != hipSuccess)
         return hip_fail(e, "hipMalloc");
     t_single.ready = true;
     return CZ_OK;
 }
 
-// NaCl box/open of one message on the device.
+static uint64_t up128(uint64_t v) { return (v + 127) & ~127ull; }
+
+// segment length for one message of nblk blocks: a lane walks seg + 1 blocks (block 0 gives its
+// Poly1305 key) and the combine lane walks the nblk / seg segments serially, so the latency is
+// ~ (seg + 1) * T_block + (nblk / seg) * T_combine, T_block / T_combine ~ 18
+static uint32_t single_seg_blocks(uint32_t nblk)
+{
+    uint32_t s = 2;
+    while ((s + 1) * (s + 1) * 18 <= nblk)
+        s++;
+    return s;
+}
+
+// NaCl box/open of one message on the device.  A MESSAGE is the NaCl box of
+// 0^32 || flags || payload, so m[32] rides as the flags byte and m[33:] as the payload; for open
+// the 16 bytes ahead of the tag are rebuilt as "\x07MESSAGE" || n[16:24] and the nonce check is off.
 static int nacl_one(uint8_t *dst, const uint8_t *src, uint64_t len, const uint8_t n[24], const uint8_t k[32],
                     int open)
 {
@@ -144,35 +159,115 @@ static int nacl_one(uint8_t *dst, const uint8_t *src, uint64_t len, const uint8_
     if (single_init() != CZ_OK)
         return -1;
     Single &s = t_single;
-    hipError_t e;
-    if ((e = s.in.reserve(len + 64)) != hipSuccess || (e = s.out.reserve(len + 64)) != hipSuccess) {
-        hip_fail(e, "hipMalloc");
-        return -1;
-    }
-    uint8_t keyblk[32];
-    memcpy(keyblk, k, 32);
     uint64_t counter = 0;
     for (int i = 0; i < 8; i++)
         counter = (counter << 8) | n[16 + i];
-    int rc = -1;
-    // HSalsa20(k, n[0:16]) on the device, then the single-frame kernel
-    if ((e = hipMemcpyAsync(s.key.ptr, keyblk, 32, hipMemcpyHostToDevice, s.stream)) != hipSuccess ||
-        (e = czk_subkeys(s.key.ptr, s.sub.ptr, 1, n, s.stream)) != hipSuccess ||
-        (e = hipMemcpyAsync(s.in.ptr, src, len, hipMemcpyHostToDevice, s.stream)) != hipSuccess ||
-        (e = czk_box_nacl(s.in.ptr, s.out.ptr, (uint32_t)len, s.sub.ptr, counter, open, (int *)s.rc.ptr,
-                          s.stream)) != hipSuccess ||
-        (e = hipMemcpyAsync(&rc, s.rc.ptr, sizeof(int), hipMemcpyDeviceToHost, s.stream)) != hipSuccess ||
+    hipError_t e;
+    if (len == 32) {  // empty box: no flags byte, so no MESSAGE form; one lane of k_box_nacl
+        uint8_t *st = nullptr;
+        if ((e = s.dev.reserve(256)) != hipSuccess || (e = s.stage.reserve(256)) != hipSuccess) {
+            hip_fail(e, "alloc");
+            return -1;
+        }
+        st = (uint8_t *)s.stage.ptr;
+        uint8_t *d = (uint8_t *)s.dev.ptr;
+        memcpy(st, k, 32);
+        memcpy(st + 128, src, 32);
+        int rc = -1;
+        if ((e = hipMemcpyAsync(d, st, 160, hipMemcpyHostToDevice, s.stream)) != hipSuccess ||
+            (e = czk_subkeys(d, d + 32, 1, n, s.stream)) != hipSuccess ||
+            (e = czk_box_nacl(d + 128, d + 192, 32, d + 32, counter, open, (int *)s.rc.ptr, s.stream)) != hipSuccess ||
+            (e = hipMemcpyAsync(st + 192, d + 192, 32, hipMemcpyDeviceToHost, s.stream)) != hipSuccess ||
+            (e = hipMemcpyAsync(&rc, s.rc.ptr, sizeof(int), hipMemcpyDeviceToHost, s.stream)) != hipSuccess ||
+            (e = hipMemsetAsync(d, 0, 64, s.stream)) != hipSuccess ||  // no key material left behind
+            (e = hipStreamSynchronize(s.stream)) != hipSuccess) {
+            memset(st, 0, 32);
+            hip_fail(e, "box");
+            return -1;
+        }
+        memset(st, 0, 32);
+        if (rc != 0)
+            return -1;
+        memcpy(dst, st + 192, 32);
+        return 0;
+    }
+    // one descriptor, its segments and combine record
+    cz_frame_desc d{};
+    d.key_idx = 0;
+    d.prev = -1;
+    if (!open) {
+        d.len = (uint32_t)(len - CZ_MESSAGE_OVERHEAD);
+        d.counter = counter;
+        d.flags = src[32];
+    } else {
+        d.len = (uint32_t)len;
+        d.counter = 0;
+        d.flags = 0;  // no replay check: a NaCl nonce is opaque
+    }
+    const uint32_t nblk = (uint32_t)((len + 63) / 64);
+    const uint32_t seg_blocks = single_seg_blocks(nblk);
+    uint32_t nseg = 0, ncomb = 0, npart = 0;
+    cz_plan_segments(&d, 1, open, seg_blocks, nullptr, 0, &nseg, nullptr, 0, &ncomb, &npart);
+    std::vector<cz_segment> seg(std::max<uint32_t>(nseg, 1));
+    std::vector<cz_combine> comb(std::max<uint32_t>(ncomb, 1));
+    if (cz_plan_segments(&d, 1, open, seg_blocks, seg.data(), (uint32_t)seg.size(), &nseg, comb.data(),
+                         (uint32_t)comb.size(), &ncomb, &npart) != CZ_OK)
+        return -1;
+    // device / staging layout: [0,32) precom [32,64) subkey [64,104) desc [128,130) status
+    // [136,144) nonce [256, ..) segments, combines | in | out | work
+    const uint64_t o_seg = 256, o_comb = o_seg + 16ull * nseg, o_in = up128(o_comb + 16ull * ncomb + 1);
+    const uint64_t in_bytes = open ? len : len - CZ_MESSAGE_OVERHEAD;
+    const uint64_t o_out = o_in + up128(in_bytes + 1), out_bytes = open ? len - CZ_MESSAGE_OVERHEAD : len;
+    const uint64_t o_work = o_out + up128(out_bytes + 1), total = o_work + 64ull * std::max<uint32_t>(npart, 1);
+    if ((e = s.dev.reserve(total)) != hipSuccess || (e = s.stage.reserve(total)) != hipSuccess) {
+        hip_fail(e, "alloc");
+        return -1;
+    }
+    uint8_t *st = (uint8_t *)s.stage.ptr, *dv = (uint8_t *)s.dev.ptr;
+    memcpy(st, k, 32);
+    d.in_off = o_in;
+    d.out_off = o_out;
+    memcpy(st + 64, &d, sizeof d);
+    memcpy(st + o_seg, seg.data(), 16ull * nseg);
+    memcpy(st + o_comb, comb.data(), 16ull * ncomb);
+    if (!open) {
+        memcpy(st + o_in, src + CZ_MESSAGE_OVERHEAD, in_bytes);
+    } else {
+        static const uint8_t hdr[8] = {7, 'M', 'E', 'S', 'S', 'A', 'G', 'E'};
+        memcpy(st + o_in, hdr, 8);
+        memcpy(st + o_in + 8, n + 16, 8);
+        memcpy(st + o_in + 16, src + 16, len - 16);
+    }
+    const cz_frame_desc *dd = (const cz_frame_desc *)(dv + 64);
+    const cz_segment *ds = (const cz_segment *)(dv + o_seg);
+    const cz_combine *dc = (const cz_combine *)(dv + o_comb);
+    if ((e = hipMemcpyAsync(dv, st, o_in + in_bytes, hipMemcpyHostToDevice, s.stream)) != hipSuccess ||
+        (e = czk_subkeys(dv, dv + 32, 1, n, s.stream)) != hipSuccess ||
+        (e = open ? czk_open_segments(dd, ds, nseg, dc, ncomb, dv, dv, dv + 32, dv + o_work, (uint16_t *)(dv + 128),
+                                      (uint64_t *)(dv + 136), s.stream)
+                  : czk_seal_segments(dd, ds, nseg, dc, ncomb, dv, dv, dv + 32, dv + o_work, s.stream)) !=
+            hipSuccess ||
+        (e = hipMemsetAsync(dv, 0, 64, s.stream)) != hipSuccess ||  // no key material left behind
+        (e = hipMemcpyAsync(st + 128, dv + 128, 2, hipMemcpyDeviceToHost, s.stream)) != hipSuccess ||
+        (e = hipMemcpyAsync(st + o_out, dv + o_out, out_bytes, hipMemcpyDeviceToHost, s.stream)) != hipSuccess ||
         (e = hipStreamSynchronize(s.stream)) != hipSuccess) {
+        memset(st, 0, 32);
         hip_fail(e, "box");
         return -1;
     }
-    if (rc != 0)
-        return -1;  // open: tag mismatch, dst untouched (as NaCl)
-    if ((e = hipMemcpyAsync(dst, s.out.ptr, len, hipMemcpyDeviceToHost, s.stream)) != hipSuccess ||
-        (e = hipStreamSynchronize(s.stream)) != hipSuccess) {
-        hip_fail(e, "box D2H");
-        return -1;
+    memset(st, 0, 32);
+    if (!open) {
+        memset(dst, 0, 16);
+        memcpy(dst + 16, st + o_out + 16, len - 16);
+        return 0;
     }
+    uint16_t status;
+    memcpy(&status, st + 128, 2);
+    if ((status & 0xff) != CZ_STATUS_OK)
+        return -1;  // tag mismatch: dst untouched (as NaCl)
+    memset(dst, 0, 32);
+    dst[32] = (uint8_t)(status >> 8);
+    memcpy(dst + 33, st + o_out, out_bytes);
     return 0;
 }
 
@@ -256,10 +351,17 @@ int cz_subkey(uint8_t out[32], const uint8_t k[32], int direction)
         return rc;
     Single &s = t_single;
     hipError_t e;
-    if ((e = hipMemcpyAsync(s.key.ptr, k, 32, hipMemcpyHostToDevice, s.stream)) != hipSuccess ||
-        (e = czk_subkeys(s.key.ptr, s.sub.ptr, 1, prefix_for(direction), s.stream)) != hipSuccess ||
-        (e = hipMemcpyAsync(out, s.sub.ptr, 32, hipMemcpyDeviceToHost, s.stream)) != hipSuccess ||
-        (e = hipStreamSynchronize(s.stream)) != hipSuccess)
+    if ((e = s.dev.reserve(256)) != hipSuccess)
+        return hip_fail(e, "hipMalloc");
+    uint8_t *d = (uint8_t *)s.dev.ptr;
+    if ((e = hipMemcpyAsync(d, k, 32, hipMemcpyHostToDevice, s.stream)) != hipSuccess ||
+        (e = czk_subkeys(d, d + 32, 1, prefix_for(direction), s.stream)) != hipSuccess ||
+        (e = hipMemcpyAsync(out, d + 32, 32, hipMemcpyDeviceToHost, s.stream)) != hipSuccess) {
+        (void)hipMemsetAsync(d, 0, 64, s.stream);
+        (void)hipStreamSynchronize(s.stream);
+        return hip_fail(e, "cz_subkey");
+    }
+    if ((e = hipMemsetAsync(d, 0, 64, s.stream)) != hipSuccess || (e = hipStreamSynchronize(s.stream)) != hipSuccess)
         return hip_fail(e, "cz_subkey");
     return CZ_OK;
 }

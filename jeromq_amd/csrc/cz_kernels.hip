@@ -1842,9 +1842,17 @@ __global__ __launch_bounds__(BLOCK) void k_open_combine(const cz_frame_desc *__r
                  ((u32)tp[4 * w + 3] << 24);
     if ((tag[0] ^ tin[0]) | (tag[1] ^ tin[1]) | (tag[2] ^ tin[2]) | (tag[3] ^ tin[3])) {
         // never release unauthenticated plaintext: zero what the segments wrote
+        // (16-byte stores over the aligned interior, bytes only at the edges: a tampered 64 KiB frame
+        // costs ~4K stores, not 64K serial byte stores)
         uint8_t *dst = out + d.out_off;
         const u32 nout = d.len - 33u;
-        for (u32 o = 0; o < nout; o++)
+        const u32 head = (u32)((16u - ((uintptr_t)dst & 15u)) & 15u);
+        u32 o = 0;
+        for (; o < head && o < nout; o++)
+            dst[o] = 0;
+        for (; o + 16u <= nout; o += 16u)
+            *reinterpret_cast<uint4 *>(dst + o) = make_uint4(0u, 0u, 0u, 0u);
+        for (; o < nout; o++)
             dst[o] = 0;
         status[cb.frame] = CZ_STATUS_CRYPTO;
     } else {

@@ -78,6 +78,8 @@ public:
     // Mechanism.encode(Msg) for one MESSAGE
     int64_t encode(const uint8_t *payload, uint64_t n, int msg_flags, uint8_t *out)
     {
+        if (n > (uint64_t)CZ_MESSAGE_MAX)
+            return fail(CZ_EMSGSIZE, "encode: %llu-byte payload exceeds CZ_MESSAGE_MAX", (unsigned long long)n);
         uint64_t in_off = 0, out_off = 0;
         uint32_t len = (uint32_t)n;
         uint8_t fl = (uint8_t)msg_flags;
@@ -92,6 +94,9 @@ public:
             return CZ_OK;
         if (!h_in || !in_off || !len || !h_out || !out_off)
             return fail(CZ_EINVAL, "encode_batch: null pointer");
+        for (uint32_t i = 0; i < count; i++)
+            if (len[i] > (uint32_t)CZ_MESSAGE_MAX)
+                return fail(CZ_EMSGSIZE, "encode_batch: frame %u (%u bytes) exceeds CZ_MESSAGE_MAX", i, len[i]);
         // device layout: 16-byte aligned frames, packed
         std::vector<cz_frame_desc> d(count);
         uint64_t ib = 0, ob = 0;
@@ -209,8 +214,8 @@ public:
             if (plen && (e = hipMemcpyAsync(h_out + out_off[i], (uint8_t *)out_.ptr + d[i].out_off, plen,
                                             hipMemcpyDeviceToHost, stream_)) != hipSuccess)
                 return hip_fail(e, "D2H");
-            if (msg_flags)
-                msg_flags[i] = (uint8_t)(st[i] >> 8);
+            if (msg_flags)  // only MORE and COMMAND reach the Msg (CurveClientMechanism.java:207-213)
+                msg_flags[i] = (uint8_t)(((st[i] >> 8) & 0x01 ? CZ_MSG_MORE : 0) | ((st[i] >> 8) & 0x02 ? CZ_MSG_COMMAND : 0));
         }
         if ((e = hipStreamSynchronize(stream_)) != hipSuccess)
             return hip_fail(e, "sync");

@@ -33,6 +33,13 @@ class CurveBatchEngine:
         except Exception:
             pass
 
+    def add_session(self, handshake):
+        """A connection from a completed CURVE handshake (jeromq_amd.handshake): its cnPrecom and nonces."""
+        rc = self._L.cz_engine_add_session(self._h, handshake._h)
+        if rc < 0:
+            _lib.check(rc, "cz_engine_add_session")
+        return rc
+
     def add_connection(self, precom, as_server=False, cn_nonce=None, cn_peer_nonce=None):
         """Per-connection CURVE state after the handshake: client MESSAGEs start at nonce 3
         and expect the server's from 2 (cn_peer_nonce 1); the server the other way round."""

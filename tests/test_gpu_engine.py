@@ -7,6 +7,7 @@ the engine must deliver exactly the payloads and flags, keep partial frames
 across reads, and tear a connection down at its first bad frame with the
 reference's event while other connections carry on.
 """
+import ctypes
 import numpy as np
 import pytest
 
@@ -173,6 +174,9 @@ def test_engine_failures_tear_down_one_connection(torch_dev, L):
     assert srv.error(sc[0]) == (0, 0) and srv.messages_in(sc[0]) == sent[0]
     assert srv.error(sc[1]) == (L.CZ_EPROTO, L.CZ_ZMTP_CRYPTOGRAPHIC)
     assert srv.messages_in(sc[1]) == sent[1][:3]
+    # the bad-tag frame passed the replay check, so cnPeerNonce = its nonce (CurveClientMechanism.java:193),
+    # as cz_mech_decode does: client nonces start at 3, frame 3 carries nonce 6
+    assert srv.peer_nonce(sc[1]) == 6 and srv.peer_nonce(sc[2]) == 5
     assert srv.error(sc[2]) == (L.CZ_EPROTO, L.CZ_ZMTP_INVALID_SEQUENCE)   # server-side replay event
     assert srv.messages_in(sc[2]) == sent[2][:3]
     assert srv.error(sc[3]) == (L.CZ_EPROTO, 0)                            # V2Decoder EPROTO, no event
@@ -180,6 +184,17 @@ def test_engine_failures_tear_down_one_connection(torch_dev, L):
     # a torn-down connection refuses further traffic; the others keep working
     assert srv.recv(sc[1], b"\x00\x01x") == L.CZ_EPROTO
     assert srv.send(sc[0], b"still fine") == 0
+
+
+def test_engine_rejects_oversized_message(torch_dev, L):
+    from jeromq_amd import _lib
+    from jeromq_amd.engine import CurveBatchEngine
+    e = CurveBatchEngine(arena_bytes=4096)
+    c = e.add_connection(PRECOM)
+    buf = ctypes.create_string_buffer(16)
+    assert _lib.lib().cz_engine_send(e._h, c, buf, L.CZ_MESSAGE_MAX + 1, 0) == L.CZ_EMSGSIZE
+    assert _lib.lib().cz_engine_send(e._h, c, buf, 0xffffffff, 0) == L.CZ_EMSGSIZE
+    assert e.send(c, b"ok") == 0
 
 
 def test_engine_zero_copy_receive_from_socket(torch_dev, L):

@@ -1,0 +1,267 @@
+"""GPU: the CURVE handshake state machine (jeromq_amd/csrc/cz_curve_hs.cpp) against libzmq 4.3.4.
+
+tests/golden/libzmq_session.json holds two live sessions (tests/golden/make_libzmq_session.py):
+  client_handshake: our client restatement against a libzmq CURVE server -- HELLO / INITIATE that
+                    libzmq accepted, WELCOME / READY that libzmq sent;
+  server_session:   a libzmq CURVE client against our server restatement -- HELLO / INITIATE that
+                    libzmq sent, WELCOME / READY that libzmq accepted, MESSAGEs both ways.
+With the short-term secret and the Curve.random() draws injected, the product state machines must
+produce the recorded commands byte for byte (CurveClientMechanism.java:246-429,
+CurveServerMechanism.java:254-517), reach READY with the recorded cnPrecom, and carry the
+recorded MESSAGE traffic through cz_mech and cz_engine.  Then product client <-> product server
+with fresh keys, and the reference's failure events."""
+import json
+import os
+import struct
+
+import pytest
+
+from cz_testlib import or_box, or_x25519, splitmix_bytes, v2_encode
+
+pytestmark = pytest.mark.gpu
+HERE = os.path.dirname(os.path.abspath(__file__))
+S = json.load(open(os.path.join(HERE, "golden", "libzmq_session.json")))
+# the reference's published CurveZMQ test keys (org/zeromq/ZMQ.java:4603-4624)
+CLIENT_PUB = bytes.fromhex("BB88471D65E2659B30C55A5321CEBB5AAB2B70A398645C26DCA2B2FCB43FC518")
+CLIENT_SEC = bytes.fromhex("7BB864B489AFA3671FBE69101F94B38972F24816DFB01B51656B3FEC8DFD0888")
+SERVER_PUB = bytes.fromhex("54FCBA24E93249969316FB617C872BB0C1D1FF14800427C594CBFACF1BC2D652")
+SERVER_SEC = bytes.fromhex("8E0BDD697628B91D8F245587EE95C5B04D48963F79259877B49CD9063AEAD3B7")
+
+
+@pytest.fixture(scope="module")
+def hs():
+    import torch
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    from jeromq_amd import handshake
+    return handshake
+
+
+def H(x):
+    return bytes.fromhex(x)
+
+
+def test_client_reproduces_libzmq_session(hs):
+    c = S["client_handshake"]
+    cli = hs.CurveClientHandshake(CLIENT_PUB, CLIENT_SEC, SERVER_PUB, ephemeral_secret=H(S["client_ephemeral_secret"]),
+                                  entropy=H(c["vouch_nonce"]))
+    assert cli.status() == hs.Status.HANDSHAKING
+    rc, hello = cli.nextHandshakeCommand()
+    assert rc == 0 and hello.data == H(c["hello"])
+    assert cli.nextHandshakeCommand() == (hs.EAGAIN, None)       # EXPECT_WELCOME: nothing to send
+    assert cli.processHandshakeCommand(H(c["welcome"])) == 0
+    rc, initiate = cli.nextHandshakeCommand()
+    assert rc == 0 and initiate.data == H(c["initiate"])
+    assert cli.status() == hs.Status.HANDSHAKING
+    assert cli.processHandshakeCommand(H(c["ready"])) == 0
+    assert cli.status() == hs.Status.READY
+    assert cli.peer_property("Socket-Type") == b"PAIR"
+    precom, n, pn = cli.session()
+    assert precom == H(S["precom"]) and n == 3 and pn == S["ready_nonce"]
+    # MESSAGE traffic on the handshake's session: the mechanism and the engine
+    mech = cli.mechanism()
+    for m in S["c2s"]:
+        from jeromq_amd.mechanism import Msg
+        assert mech.encode(Msg(splitmix_bytes(m["n"], m["seed"]), m["flags"])).data.hex() == m["body"]
+    from jeromq_amd.engine import CurveBatchEngine
+    eng = CurveBatchEngine(arena_bytes=1 << 20)
+    conn = eng.add_session(cli)
+    eng.recv(conn, H(S["s2c_wire"]))
+    eng.flush_in()
+    assert eng.error(conn) == (0, 0)
+    assert eng.messages_in(conn) == [(splitmix_bytes(m["n"], m["seed"]), m["flags"]) for m in S["s2c"]]
+    for m in S["c2s"]:
+        eng.send(conn, splitmix_bytes(m["n"], m["seed"]), more=bool(m["flags"] & 1))
+    eng.flush_out()
+    assert eng.wire_out(conn) == b"".join(v2_encode(H(m["body"])) for m in S["c2s"])
+
+
+def test_server_reproduces_libzmq_session(hs):
+    s = S["server_session"]
+    srv = hs.CurveServerHandshake(SERVER_SEC, ephemeral_secret=H(s["server_ephemeral_secret"]), entropy=H(s["entropy"]))
+    assert srv.nextHandshakeCommand() == (hs.EAGAIN, None)       # EXPECT_HELLO
+    assert srv.processHandshakeCommand(H(s["hello"])) == 0
+    rc, welcome = srv.nextHandshakeCommand()
+    assert rc == 0 and welcome.data == H(s["welcome"])
+    assert srv.processHandshakeCommand(H(s["initiate"])) == 0
+    assert srv.client_key() == CLIENT_PUB
+    assert srv.peer_property("Socket-Type") == b"PAIR"
+    rc, ready = srv.nextHandshakeCommand()
+    assert rc == 0 and ready.data == H(s["ready"])
+    assert srv.status() == hs.Status.READY
+    precom, n, pn = srv.session()
+    assert precom == H(s["precom"]) and n == 2 and pn == 2
+    mech = srv.mechanism()
+    from jeromq_amd.mechanism import Msg
+    for m in s["c2s"]:      # libzmq client's MESSAGEs
+        got = mech.decode(Msg(H(m["body"])))
+        assert got is not None and got.data == splitmix_bytes(m["n"], m["seed"]) and got.flags == m["flags"]
+    for m in s["s2c"]:      # what libzmq's client opened
+        assert mech.encode(Msg(splitmix_bytes(m["n"], m["seed"]), m["flags"])).data.hex() == m["body"]
+
+
+def run_handshake(hs, cli, srv):
+    """Move commands until neither side has one to send (the StreamEngine handshake loop)"""
+    for _ in range(8):
+        moved = False
+        for a, b in ((cli, srv), (srv, cli)):
+            rc, cmd = a.nextHandshakeCommand()
+            if rc == 0:
+                moved = True
+                r = b.processHandshakeCommand(cmd)
+                if r != 0:
+                    return r, b
+        if not moved:
+            break
+    return 0, None
+
+
+def test_product_client_server(hs):
+    from jeromq_amd.mechanism import Msg
+    cli = hs.CurveClientHandshake(CLIENT_PUB, CLIENT_SEC, SERVER_PUB, socket_type=hs.ZMQ_DEALER, identity=b"peer-7")
+    srv = hs.CurveServerHandshake(SERVER_SEC, socket_type=hs.ZMQ_ROUTER, identity=b"")
+    assert run_handshake(hs, cli, srv) == (0, None)
+    assert cli.status() == srv.status() == hs.Status.READY
+    assert srv.peer_property("Identity") == b"peer-7" and srv.peer_property("Socket-Type") == b"DEALER"
+    assert cli.peer_property("Socket-Type") == b"ROUTER" and cli.peer_property("Identity") == b""
+    assert srv.client_key() == CLIENT_PUB
+    kc, nc, pc = cli.session()
+    ks, ns, ps = srv.session()
+    assert kc == ks and (nc, pc, ns, ps) == (3, 1, 2, 2)
+    mc, ms = cli.mechanism(), srv.mechanism()
+    for i in range(5):
+        p = splitmix_bytes(37 * i, 900 + i)
+        got = ms.decode(mc.encode(Msg(p, i & 1)))
+        assert got.data == p and got.flags == (i & 1)
+        got = mc.decode(ms.encode(Msg(p[::-1])))
+        assert got.data == p[::-1]
+
+
+def test_client_failure_events(hs):
+    c = S["client_handshake"]
+    eph = H(S["client_ephemeral_secret"])
+    mk = lambda: hs.CurveClientHandshake(CLIENT_PUB, CLIENT_SEC, SERVER_PUB, ephemeral_secret=eph,  # noqa: E731
+                                         entropy=H(c["vouch_nonce"]))
+    w = bytearray(H(c["welcome"]))
+    cli = mk()
+    cli.nextHandshakeCommand()
+    w[100] ^= 1
+    assert cli.processHandshakeCommand(bytes(w)) == hs.EPROTO
+    assert cli.last_event == 0x11000001                               # ZMTP_CRYPTOGRAPHIC
+    cli = mk()
+    cli.nextHandshakeCommand()
+    assert cli.processHandshakeCommand(H(c["welcome"])[:167]) == hs.EPROTO
+    assert cli.last_event == 0x10000016                               # MALFORMED_COMMAND_READY (sic)
+    assert cli.processHandshakeCommand(b"\x05HELLO" + bytes(10)) == hs.EPROTO
+    assert cli.last_event == 0x10000001                               # UNEXPECTED_COMMAND
+    # READY with a flipped box byte, and a short READY
+    cli = mk()
+    cli.nextHandshakeCommand()
+    cli.processHandshakeCommand(H(c["welcome"]))
+    cli.nextHandshakeCommand()
+    r = bytearray(H(c["ready"]))
+    r[-1] ^= 0x80
+    assert cli.processHandshakeCommand(bytes(r)) == hs.EPROTO and cli.last_event == 0x11000001
+    assert cli.processHandshakeCommand(H(c["ready"])[:29]) == hs.EPROTO and cli.last_event == 0x10000016
+    # ERROR from the server while waiting: status ERROR (processError, parseErrorMessage)
+    assert cli.processHandshakeCommand(b"\x05ERROR\x03400") == 0
+    assert cli.status() == hs.Status.ERROR
+    cli = mk()
+    assert cli.processHandshakeCommand(b"\x05ERROR\x00") == hs.EPROTO  # SEND_HELLO: unexpected ERROR
+    assert cli.last_event == 0x10000001
+    cli = mk()
+    cli.nextHandshakeCommand()
+    assert cli.processHandshakeCommand(b"\x05ERROR\x05ab") == hs.EPROTO  # reason longer than the frame
+    assert cli.last_event == 0x10000015
+
+
+def test_server_failure_events(hs):
+    s = S["server_session"]
+    mk = lambda **kw: hs.CurveServerHandshake(SERVER_SEC, ephemeral_secret=H(s["server_ephemeral_secret"]),  # noqa
+                                              entropy=H(s["entropy"]), **kw)
+    # HELLO with a bad box: the server answers ERROR with an empty status code
+    srv = mk()
+    h = bytearray(H(s["hello"]))
+    h[150] ^= 1
+    assert srv.processHandshakeCommand(bytes(h)) == 0 and srv.last_event == 0x11000001
+    rc, err = srv.nextHandshakeCommand()
+    assert rc == 0 and err.data == b"\x05ERROR\x00" and srv.status() == hs.Status.ERROR
+    srv = mk()
+    assert srv.processHandshakeCommand(H(s["hello"])[:199]) == hs.EPROTO and srv.last_event == 0x10000013
+    srv = mk()
+    h = bytearray(H(s["hello"]))
+    h[6] = 2                                                           # version 2.0
+    assert srv.processHandshakeCommand(bytes(h)) == hs.EPROTO and srv.last_event == 0x10000013
+    srv = mk()
+    assert srv.processHandshakeCommand(H(s["initiate"])) == hs.EPROTO and srv.last_event == 0x10000001
+    # INITIATE: bad cookie, short, tampered box
+    for mutate, ev in ((lambda b: b.__setitem__(30, b[30] ^ 1), 0x11000001),
+                       (lambda b: b.__setitem__(200, b[200] ^ 1), 0x11000001)):
+        srv = mk()
+        srv.processHandshakeCommand(H(s["hello"]))
+        srv.nextHandshakeCommand()
+        i = bytearray(H(s["initiate"]))
+        mutate(i)
+        assert srv.processHandshakeCommand(bytes(i)) == hs.EPROTO and srv.last_event == ev
+    srv = mk()
+    srv.processHandshakeCommand(H(s["hello"]))
+    srv.nextHandshakeCommand()
+    assert srv.processHandshakeCommand(H(s["initiate"])[:256]) == hs.EPROTO and srv.last_event == 0x10000014
+    # a command after CONNECTED: ZMTP_UNSPECIFIED
+    srv = mk()
+    srv.processHandshakeCommand(H(s["hello"]))
+    srv.nextHandshakeCommand()
+    srv.processHandshakeCommand(H(s["initiate"]))
+    srv.nextHandshakeCommand()
+    assert srv.processHandshakeCommand(H(s["hello"])) == hs.EPROTO and srv.last_event == 0x10000000
+
+
+def test_vouch_mismatch_and_socket_types(hs):
+    """An INITIATE whose vouch names another short-term key -> KEY_EXCHANGE; incompatible
+    Socket-Type -> EINVAL (parseMetadata)."""
+    eph_c = bytes(range(0x10, 0x30))
+    cli_pub_eph = or_x25519(eph_c, (9).to_bytes(32, "little"))
+    srv = hs.CurveServerHandshake(SERVER_SEC)
+    hello_box = or_box(bytes(64), b"CurveZMQHELLO---" + struct.pack(">Q", 1), SERVER_PUB, eph_c)[16:]
+    hello = b"\x05HELLO\x01\x00" + bytes(72) + cli_pub_eph + struct.pack(">Q", 1) + hello_box
+    assert srv.processHandshakeCommand(hello) == 0
+    rc, welcome = srv.nextHandshakeCommand()
+    from cz_testlib import oracle
+    import ctypes
+    k = ctypes.create_string_buffer(32)
+    oracle().or_box_beforenm(k, SERVER_PUB, eph_c)
+    wc = bytes(16) + welcome.data[24:168]
+    wp = ctypes.create_string_buffer(len(wc))
+    assert oracle().or_secretbox_open(wp, wc, len(wc), b"WELCOME-" + welcome.data[8:24], k.raw) == 0
+    srv_eph, cookie = wp.raw[32:64], wp.raw[64:160]
+    vn = bytes(16)
+    vouch = or_box(bytes(32) + SERVER_PUB, b"VOUCH---" + vn, srv_eph, CLIENT_SEC)[16:]   # wrong C' inside
+    meta = bytes([11]) + b"Socket-Type" + struct.pack(">I", 4) + b"PAIR"
+    ibox = or_box(CLIENT_PUB + vn + vouch + meta, b"CurveZMQINITIATE" + struct.pack(">Q", 2), srv_eph, eph_c)[16:]
+    assert srv.processHandshakeCommand(b"\x08INITIATE" + cookie + struct.pack(">Q", 2) + ibox) == hs.EPROTO
+    assert srv.last_event == 0x10000003                                # ZMTP_KEY_EXCHANGE
+    # PUB client against a PAIR server: the server's parseMetadata rejects the Socket-Type
+    cli = hs.CurveClientHandshake(CLIENT_PUB, CLIENT_SEC, SERVER_PUB, socket_type=hs.ZMQ_PUB)
+    srv = hs.CurveServerHandshake(SERVER_SEC, socket_type=hs.ZMQ_PAIR)
+    rc, side = run_handshake(hs, cli, srv)
+    assert rc == hs.EINVAL and side is srv
+
+
+def test_zap_flow(hs):
+    for code, want in (("200", hs.Status.READY), ("400", hs.Status.ERROR)):
+        cli = hs.CurveClientHandshake(CLIENT_PUB, CLIENT_SEC, SERVER_PUB)
+        srv = hs.CurveServerHandshake(SERVER_SEC, zap=True)
+        assert run_handshake(hs, cli, srv) == (0, None)
+        assert srv.status() == hs.Status.HANDSHAKING                  # EXPECT_ZAP_REPLY
+        assert srv.nextHandshakeCommand() == (hs.EAGAIN, None)
+        assert srv.client_key() == CLIENT_PUB                          # what the ZAP request carries
+        assert srv.zapReply(code) == 0
+        rc, cmd = srv.nextHandshakeCommand()
+        assert rc == 0
+        if code == "200":
+            assert cmd.data[:6] == b"\x05READY"
+            assert cli.processHandshakeCommand(cmd) == 0 and cli.status() == hs.Status.READY
+        else:
+            assert cmd.data == b"\x05ERROR\x03400"
+            assert cli.processHandshakeCommand(cmd) == 0 and cli.status() == hs.Status.ERROR
+        assert srv.status() == want

@@ -383,6 +383,40 @@ def test_nacl_box_afternm_golden(L, torch_dev):
     assert cv.afternm(bytearray(31), bytes(31), 31, bytes(24), bytes(32)) == -1
 
 
+def test_nacl_single_shot_multi_lane(L, torch_dev):
+    """The jnacl drop-ins (Curve.java:129-147) for one message of any size: large boxes run through the
+    segment kernels (many lanes); every byte and tag against the oracle (NaCl secretbox), m[32] any
+    byte value, tampering anywhere -> -1 with the output buffer untouched."""
+    from cz_testlib import or_box_afternm
+    lib = L.lib()
+    rng = np.random.default_rng(77)
+    for mlen in (32, 33, 34, 63, 64, 95, 96, 97, 160, 1000, 4128, 4129, 16416, 65568, 65568 + 33 + 64 * 7, 200003):
+        key = rng.integers(0, 256, 32, dtype=np.uint8).tobytes()
+        n24 = rng.integers(0, 256, 24, dtype=np.uint8).tobytes()
+        m = bytes(32) + rng.integers(0, 256, mlen - 32, dtype=np.uint8).tobytes()
+        rc, want = or_box_afternm(m, n24, key)
+        assert rc == 0
+        c = ctypes.create_string_buffer(mlen)
+        assert lib.cz_box_afternm(c, m, mlen, n24, key) == 0, mlen
+        assert c.raw == want, f"box mismatch at mlen={mlen}"
+        c2 = ctypes.create_string_buffer(mlen)
+        assert lib.cz_secretbox(c2, m, mlen, n24, key) == 0 and c2.raw == want
+        out = ctypes.create_string_buffer(mlen)
+        assert lib.cz_box_open_afternm(out, want, mlen, n24, key) == 0 and out.raw == m, mlen
+        for pos in sorted({16, 31, 32, mlen - 1, (mlen + 32) // 2}):
+            if pos >= mlen:
+                continue
+            bad = bytearray(want)
+            bad[pos] ^= 0x40
+            sentinel = ctypes.create_string_buffer(b"\xaa" * mlen, mlen)
+            assert lib.cz_secretbox_open(sentinel, bytes(bad), mlen, n24, key) == -1, (mlen, pos)
+            assert sentinel.raw == b"\xaa" * mlen
+        # bytes 0..15 of c are not authenticated (NaCl ignores them)
+        junk = bytearray(want)
+        junk[:16] = b"\x55" * 16
+        assert lib.cz_box_open_afternm(out, bytes(junk), mlen, n24, key) == 0 and out.raw == m
+
+
 def test_mechanism_client_server(L, torch_dev):
     from jeromq_amd.mechanism import CurveClientMechanism, CurveServerMechanism, Msg
     cli = CurveClientMechanism(PRECOM)
@@ -408,6 +442,30 @@ def test_mechanism_client_server(L, torch_dev):
     assert cli.decode(Msg(b"\x07MESSAGE" + bytes(10))) is None
     assert cli.last_event == L.CZ_ZMTP_MALFORMED_COMMAND_MESSAGE
     assert cli.decode(Msg(b"\x05READY" + bytes(40))) is None and cli.last_event == L.CZ_ZMTP_UNEXPECTED_COMMAND
+
+
+def test_mechanism_limits_and_flags(L, torch_dev):
+    """oversized payloads are refused before any device work (a u32 mlen would wrap), and
+    decode / decodeBatch map the decrypted flags byte to MORE | COMMAND only, as the reference does
+    (CurveClientMechanism.java:207-213) -- a 0xff flags byte gives MORE | COMMAND, not 0xff."""
+    import ctypes
+    from jeromq_amd import _lib
+    from jeromq_amd.mechanism import CurveClientMechanism, CurveServerMechanism, Msg
+    cli = CurveClientMechanism(PRECOM)
+    srv = CurveServerMechanism(PRECOM)
+    buf = ctypes.create_string_buffer(64)
+    assert _lib.lib().cz_mech_encode(cli._h, buf, L.CZ_MESSAGE_MAX + 1, 0, buf) == L.CZ_EMSGSIZE
+    assert _lib.lib().cz_mech_encode(cli._h, buf, 1 << 32, 0, buf) == L.CZ_EMSGSIZE
+    lens = (ctypes.c_uint32 * 2)(3, 0xffffffff)
+    offs = (ctypes.c_uint64 * 2)(0, 0)
+    assert _lib.lib().cz_mech_encode_batch(cli._h, 2, buf, offs, lens, None, buf, offs) == L.CZ_EMSGSIZE
+    assert cli.cnNonce == 3                                   # nothing was sealed
+    body = or_curve_encode(b"payload", 0xff, 3, 0, PRECOM)    # flags byte 0xff from a foreign peer
+    got = srv.decode(Msg(body))
+    assert got.data == b"payload" and got.flags == Msg.MORE | Msg.COMMAND
+    srv2 = CurveServerMechanism(PRECOM)
+    got = srv2.decodeBatch([Msg(body), Msg(or_curve_encode(b"x", 0xfc, 4, 0, PRECOM))])
+    assert [g.flags for g in got] == [Msg.MORE | Msg.COMMAND, 0]
 
 
 def test_mechanism_batches(L, torch_dev):

@@ -572,6 +572,19 @@ def main():
     kern_ms = [a.elapsed_time(b) for a, b in evs]
     avg_kernel_s = float(np.mean(kern_ms)) / 1e3
 
+    per_rank = None
+    if world > 1:
+        # every rank's own kernel time and roofline fraction (the driver's 1/2/4/8-GPU runs then
+        # carry absolute per-GPU figures with no further code change)
+        import torch.distributed as dist
+        kd = "cuda" if dist.get_backend() == "nccl" else "cpu"
+        mine = torch.tensor([avg_kernel_s], dtype=torch.float64, device=kd)
+        allk = [torch.zeros(1, dtype=torch.float64, device=kd) for _ in range(world)]
+        dist.all_gather(allk, mine)
+        alg = wl.read_bytes + wl.write_bytes
+        per_rank = [{"rank": r, "kernel_ms": round(float(k.item()) * 1e3, 4),
+                     "payload_GiBps": round(wl.payload_bytes / float(k.item()) / 2**30, 2),
+                     "hbm_frac": round(alg / float(k.item()) / 1e9 / HBM_PEAK_GBS, 4)} for r, k in enumerate(allk)]
     elapsed = max_over_ranks(world, elapsed)
     total_payload = sum_over_ranks(world, float(wl.payload_bytes) * args.steps)
     value = total_payload / elapsed / 2**30
@@ -614,12 +627,13 @@ def main():
             "config": {"workload": names[args.config], "frames_per_gpu": wl.count,
                        "payload_bytes_per_gpu": wl.payload_bytes, "parallelism": f"shard{world}",
                        "frames_per_s": round(wl.count * world * args.steps / elapsed, 1)},
-            "roofline": {"bound": "hbm", "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+            # bound: the roof that binds is VALU issue; achieved / peak / frac are the
+            # HBM figures the north star asks for, the VALU roof is in "valu"
+            "roofline": {"bound": "valu", "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": round(achieved / HBM_PEAK_GBS, 4),
                          "traffic": traffic,
                          "kernel_ms": round(avg_kernel_s * 1e3, 4),
                          "alg_bytes_per_launch": alg_bytes,
-                         # the roof that binds: VALU issue
                          "valu": valu_roofline(pmc, avg_kernel_s)},
             "cpu_baseline": cpu,
         }
@@ -627,6 +641,8 @@ def main():
             line["seal_open_verify"] = rtl
         if sg is not None:
             line["scatter_gather"] = sg
+        if per_rank is not None:
+            line["per_rank"] = per_rank
         print(json.dumps(line), flush=True)
     if world > 1:
         import torch.distributed as dist

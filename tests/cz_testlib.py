@@ -213,3 +213,42 @@ def or_box(m, n24, pk, sk):
     c = ctypes.create_string_buffer(len(mm))
     assert oracle().or_secretbox(c, mm, len(mm), bytes(n24), k) == 0
     return c.raw
+
+
+def oracle_check_full(d_in, d_out, desc, precom, from_server=0, chunk_bytes=256 << 20, threads=None):
+    """Every frame of a device-sealed batch against the oracle (or_seal_batch), byte for byte.
+
+    d_in / d_out: torch uint8 device tensors holding payloads / bodies at desc's offsets (desc: a
+    DESC_DTYPE array, frames in increasing offset order).  The batch is checked in chunks of about
+    chunk_bytes of output, so a 4 GiB batch needs ~2 x chunk_bytes of host memory.  The oracle
+    writes its bodies over a copy of the device's chunk, so only body bytes are compared (slot
+    padding belongs to the caller's layout).  Returns the number of frames checked."""
+    import os as _os
+    if threads is None:
+        threads = max(1, min(16, _os.cpu_count() or 1))
+    n = len(desc)
+    blen = desc["len"].astype(np.uint64) + np.uint64(33)
+    pk = np.frombuffer(bytes(precom), dtype=np.uint8).copy()
+    a = 0
+    while a < n:
+        o0 = int(desc["out_off"][a])
+        b = int(np.searchsorted(desc["out_off"], np.uint64(o0 + chunk_bytes), side="left"))
+        b = max(b, a + 1)
+        i0 = int(desc["in_off"][a])
+        i1 = int((desc["in_off"][a:b] + desc["len"][a:b].astype(np.uint64)).max())
+        o1 = int((desc["out_off"][a:b] + blen[a:b]).max())
+        hin = d_in[i0:max(i1, i0 + 1)].cpu().numpy()
+        got = d_out[o0:o1].cpu().numpy()
+        want = got.copy()
+        cd = desc[a:b].copy()
+        cd["in_off"] -= np.uint64(i0)
+        cd["out_off"] -= np.uint64(o0)
+        oracle().or_seal_batch(cd.ctypes.data, b - a, hin.ctypes.data, want.ctypes.data, pk.ctypes.data,
+                               from_server, threads)
+        if not np.array_equal(got, want):
+            for k in range(a, b):
+                s0, s1 = int(cd["out_off"][k - a]), int(cd["out_off"][k - a] + blen[k])
+                if not np.array_equal(got[s0:s1], want[s0:s1]):
+                    raise AssertionError(f"frame {k} (len {int(desc['len'][k])}) differs from the oracle")
+        a = b
+    return n

@@ -6,6 +6,7 @@ is not vendored and no JDK exists in this image.  The reference's own tests hold
 no crypto known-answer vectors; the RFC test keys they use
 (org/zeromq/ZMQ.java:4603-4624) drive the MESSAGE vectors here.
 """
+import numpy as np
 import pytest
 
 from cz_testlib import (load_golden, or_box_afternm, or_box_open_afternm, or_curve_decode, or_curve_encode,
@@ -92,3 +93,28 @@ def test_decode_rejects_malformed():
     bad = bytearray(body)
     bad[20] ^= 1
     assert or_curve_decode(bytes(bad), 0, K)[0] == 1
+
+
+def test_oracle_check_full_helper():
+    """The full-batch checker the GPU parity tests use (cz_testlib.oracle_check_full), exercised on
+    CPU tensors: it accepts an oracle-sealed batch in several chunks and names a corrupted frame."""
+    import torch
+    from cz_testlib import DESC_DTYPE, oracle_check_full, or_curve_encode, splitmix_bytes
+    key = bytes(range(32))
+    lens = [0, 1, 100, 4096, 5000, 31, 64]
+    desc = np.zeros(len(lens), dtype=DESC_DTYPE)
+    io = oo = 0
+    hin, hout = bytearray(), bytearray()
+    for i, n in enumerate(lens):
+        p = splitmix_bytes(n, 300 + i)
+        desc[i] = (io, oo, n, 0, 3 + i, i & 3, -1)
+        hin += p + bytes((-n) % 16)
+        body = or_curve_encode(p, i & 3, 3 + i, 0, key)
+        hout += body + bytes((-len(body)) % 128)
+        io, oo = len(hin), len(hout)
+    d_in = torch.frombuffer(bytearray(hin + bytes(16)), dtype=torch.uint8)
+    d_out = torch.frombuffer(bytearray(hout), dtype=torch.uint8)
+    assert oracle_check_full(d_in, d_out, desc, key, chunk_bytes=300) == len(lens)
+    d_out[int(desc["out_off"][4]) + 2000] ^= 1
+    with pytest.raises(AssertionError, match="frame 4"):
+        oracle_check_full(d_in, d_out, desc, key, chunk_bytes=300)

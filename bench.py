@@ -49,7 +49,8 @@ def parse():
                     help="zipf: input payload slot alignment in bytes (lengths are 64-byte multiples)")
     ap.add_argument("--out-align", type=int, default=128,
                     help="zipf: output slot alignment in bytes (the caller's packing choice)")
-    ap.add_argument("--config", default="4k", choices=["4k", "100b", "zipf", "zipf_lane", "open4k", "e2e4k", "engine", "beforenm"])
+    ap.add_argument("--config", default="4k", choices=["4k", "4k_dense", "100b", "zipf", "zipf_lane", "open4k", "e2e4k", "engine",
+                                                          "beforenm"])
     ap.add_argument("--frames", type=int, default=FRAMES)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-scatter", action="store_true",
@@ -114,7 +115,7 @@ def shard_plan(rank, frames_per_rank, cfg="4k"):
     """Rank r seals frames [r*F, (r+1)*F) of the global batch: nonce counters 3 + r*F ..,
     its own payload seed.  Frames are independent, so no data crosses ranks (weak scaling)."""
     counter0 = 3 + rank * frames_per_rank
-    seed = 0x5EED0000 + {"4k": 1, "100b": 2, "zipf": 3, "zipf_lane": 3, "open4k": 4}[cfg] + 1000 * rank
+    seed = 0x5EED0000 + {"4k": 1, "4k_dense": 1, "100b": 2, "zipf": 3, "zipf_lane": 3, "open4k": 4}[cfg] + 1000 * rank
     return counter0, seed
 
 
@@ -128,13 +129,15 @@ class Workload:
         self.subkey = batch.subkeys(key, _lib.CZ_DIR_C2S)[0].contiguous()
         self.counter0, seed = shard_plan(rank, frames, cfg)
         self.count = frames
-        if cfg in ("4k", "100b", "open4k"):
+        if cfg in ("4k", "4k_dense", "100b", "open4k"):
             n = 4096 if cfg != "100b" else 100
             self.n = n
             self.in_stride = (n + 15) // 16 * 16
             # 4 KiB: 128-byte body slots (full-line LDS-staged stores); 100 B: dense 16-byte slots
             # (64 slots fit the LDS region stager)
             self.out_stride = (n + 33 + 127) // 128 * 128 if n >= 1024 else (n + 33 + 15) // 16 * 16
+            if cfg == "4k_dense":  # bodies back to back (4129-byte slots), as the wire packs them
+                self.out_stride = n + 33
             self.d_in = torch.empty(frames * self.in_stride, dtype=torch.uint8, device=dev)
             batch.fill(self.d_in, seed)
             self.flags = torch.zeros(frames, dtype=torch.uint8, device=dev)
@@ -196,7 +199,7 @@ class Workload:
         torch.cuda.synchronize()
 
     def step(self):
-        if self.cfg in ("4k", "100b"):
+        if self.cfg in ("4k", "4k_dense", "100b"):
             batch.seal_uniform(self.d_in, self.in_stride, self.d_out, self.out_stride, self.count, self.n,
                                self.subkey, self.counter0, flags8=self.flags)
         elif self.cfg == "open4k":
@@ -213,8 +216,8 @@ class Workload:
         sys.path.insert(0, os.path.join(ROOT, "tests"))
         from cz_testlib import or_curve_encode
         torch.cuda.synchronize()
-        if self.cfg in ("4k", "100b"):
-            for i in (0, 7, self.count // 2, self.count - 1):
+        if self.cfg in ("4k", "4k_dense", "100b"):
+            for i in (0, 1, 7, self.count // 2, self.count - 2, self.count - 1):
                 p = self.d_in[i * self.in_stride:i * self.in_stride + self.n].cpu().numpy().tobytes()
                 body = self.d_out[i * self.out_stride:i * self.out_stride + self.n + 33].cpu().numpy().tobytes()
                 fl = 1 if i % 8 == 0 else 0
@@ -606,7 +609,9 @@ def main():
         cpu = cpu_baseline(wl, args.cpu_seconds)
 
     if rank == 0:
-        names = {"4k": "1M x 4 KiB frames, seal (configs[1])", "100b": "1M x 100 B frames, seal (configs[2])",
+        names = {"4k": "1M x 4 KiB frames, seal (configs[1])",
+                 "4k_dense": "1M x 4 KiB frames, seal, bodies packed back to back (4129-byte slots)",
+                 "100b": "1M x 100 B frames, seal (configs[2])",
                  "zipf": "1M Zipf(1.2) 64 B..64 KiB frames, seal, segmented (configs[3])",
                  "zipf_lane": "1M Zipf(1.2) 64 B..64 KiB frames, seal, lane per frame (configs[3])",
                  "open4k": "1M x 4 KiB frames, open+verify (configs[4] leg)"}

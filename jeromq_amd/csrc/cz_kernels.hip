@@ -89,6 +89,54 @@ struct V4 {
 
 __device__ __forceinline__ V4 zero4() { return V4{0u, 0u, 0u, 0u}; }
 
+// Byte-granular pieces of a 16-byte unit.  gfx950 executes unaligned global and LDS
+// accesses (the compiler emits them for align-1 types), so a clipped edge unit leaves in at
+// most 4 stores (8, 4, 2, 1 bytes) instead of a byte loop.
+typedef uint64_t u64_ua __attribute__((aligned(1)));
+typedef uint32_t u32_ua __attribute__((aligned(1)));
+typedef uint16_t u16_ua __attribute__((aligned(1)));
+struct __attribute__((packed)) U16ua {
+    uint4 v;
+};
+
+// store bytes [a, b) (0 <= a <= b <= 16) of the unit v whose byte 0 belongs at p
+__device__ void st_range16(uint8_t *p, uint4 v, u32 a, u32 b)
+{
+    if (b <= a)
+        return;
+    u64 lo = ((u64)v.y << 32) | v.x, hi = ((u64)v.w << 32) | v.z;
+    if (a >= 8u) {
+        lo = hi >> (8u * (a - 8u));
+        hi = 0;
+    } else if (a) {
+        lo = (lo >> (8u * a)) | (hi << (64u - 8u * a));
+        hi >>= 8u * a;
+    }
+    uint8_t *q = p + a;
+    const u32 n = b - a;
+    if (n == 16u) {
+        reinterpret_cast<U16ua *>(q)->v = v;
+        return;
+    }
+    if (n & 8u) {
+        *reinterpret_cast<u64_ua *>(q) = lo;
+        q += 8;
+        lo = hi;
+    }
+    if (n & 4u) {
+        *reinterpret_cast<u32_ua *>(q) = (u32)lo;
+        q += 4;
+        lo >>= 32;
+    }
+    if (n & 2u) {
+        *reinterpret_cast<u16_ua *>(q) = (uint16_t)lo;
+        q += 2;
+        lo >>= 16;
+    }
+    if (n & 1u)
+        *q = (uint8_t)lo;
+}
+
 // Load 16 bytes from p.  avail = bytes of the object remaining at p.
 // AL: p is 16-byte aligned, so reading the whole aligned chunk once any byte of
 // it is valid cannot cross a page; bytes past the object are ignored by callers.
@@ -101,6 +149,10 @@ __device__ __forceinline__ V4 ld16(const uint8_t *__restrict__ p, u64 avail)
         uint4 v = *reinterpret_cast<const uint4 *>(p);
         return V4{v.x, v.y, v.z, v.w};
     } else {
+        if (avail >= 16u) {  // every byte valid: one unaligned load (cannot touch an unmapped page)
+            const uint4 v = reinterpret_cast<const U16ua *>(p)->v;
+            return V4{v.x, v.y, v.z, v.w};
+        }
         u32 w[4] = {0u, 0u, 0u, 0u};
         u32 lim = avail < 16 ? (u32)avail : 16u;
         for (u32 i = 0; i < lim; i++)
@@ -149,19 +201,20 @@ __device__ __forceinline__ void st16(uint8_t *__restrict__ p, u32 a, u32 b, u32 
     if constexpr (AL) {
         *reinterpret_cast<uint4 *>(p) = make_uint4(a, b, c, d);
     } else {
-        u32 w[4] = {a, b, c, d};
-#pragma unroll
-        for (int i = 0; i < 16; i++)
-            p[i] = (uint8_t)(w[i >> 2] >> (8 * (i & 3)));
+        reinterpret_cast<U16ua *>(p)->v = make_uint4(a, b, c, d);
     }
 }
 
 // Store the first nb (0..16) bytes of a 16-byte chunk.
 __device__ __forceinline__ void st_bytes(uint8_t *__restrict__ p, u32 a, u32 b, u32 c, u32 d, u32 nb)
 {
+#ifdef CZ_XP_BYTE_LOOP
     u32 w[4] = {a, b, c, d};
     for (u32 i = 0; i < nb; i++)
         p[i] = (uint8_t)(w[i >> 2] >> (8 * (i & 3)));
+#else
+    st_range16(p, make_uint4(a, b, c, d), 0u, nb);
+#endif
 }
 
 __device__ __forceinline__ u32 funnel(u32 hi, u32 lo, u32 sh) { return __builtin_amdgcn_alignbyte(hi, lo, sh); }
@@ -977,6 +1030,221 @@ __device__ __forceinline__ u64 read_be64(const uint8_t *p)
 // the same chunk count can share the cooperative line emitter below.
 // ---------------------------------------------------------------------------
 
+// Stores through pointers rebuilt from integers (ds_bpermute'd bases) would compile to flat_*
+// instructions, which also count against lgkmcnt: every LDS wait of the emitter would then
+// wait for them too.  These go out as global_* stores.
+typedef unsigned v4u_t __attribute__((ext_vector_type(4)));
+typedef __attribute__((address_space(1))) v4u_t g_uint4;
+typedef __attribute__((address_space(1))) uint8_t g_u8;
+typedef __attribute__((address_space(1))) u64_ua g_u64_ua;
+typedef __attribute__((address_space(1))) u32_ua g_u32_ua;
+typedef __attribute__((address_space(1))) u16_ua g_u16_ua;
+typedef v4u_t v4u_ua __attribute__((aligned(1)));
+typedef __attribute__((address_space(1))) v4u_ua g_v4u_ua;
+
+// bytes [a, b) of unit v at global address p (st_range16 for a global pointer); out of line:
+// only an output's edge units take it
+__device__ __noinline__ void st_range16_g(u64 p, uint4 v, u32 a, u32 b)
+{
+    if (b <= a)
+        return;
+    u64 lo = ((u64)v.y << 32) | v.x, hi = ((u64)v.w << 32) | v.z;
+    if (a >= 8u) {
+        lo = hi >> (8u * (a - 8u));
+        hi = 0;
+    } else if (a) {
+        lo = (lo >> (8u * a)) | (hi << (64u - 8u * a));
+        hi >>= 8u * a;
+    }
+    u64 q = p + a;
+    const u32 n = b - a;
+    if (n == 16u) {
+        *reinterpret_cast<g_v4u_ua *>(q) = v4u_t{v.x, v.y, v.z, v.w};
+        return;
+    }
+    if (n & 8u) {
+        *reinterpret_cast<g_u64_ua *>(q) = lo;
+        q += 8;
+        lo = hi;
+    }
+    if (n & 4u) {
+        *reinterpret_cast<g_u32_ua *>(q) = (u32)lo;
+        q += 4;
+        lo >>= 32;
+    }
+    if (n & 2u) {
+        *reinterpret_cast<g_u16_ua *>(q) = (uint16_t)lo;
+        q += 2;
+        lo >>= 16;
+    }
+    if (n & 1u)
+        *reinterpret_cast<g_u8 *>(q) = (uint8_t)lo;
+}
+
+// unit v at global address p clipped to its bytes [a, b), minus [t0, t1) when t1 > t0
+__device__ __noinline__ void st_unit_clip(u64 p, uint4 v, u32 a, u32 b, u32 t0, u32 t1)
+{
+    if (t1 > t0) {
+        st_range16_g(p, v, a, b < t0 ? b : t0);
+        st_range16_g(p, v, a > t1 ? a : t1, b);
+    } else {
+        st_range16_g(p, v, a, b);
+    }
+}
+
+// zero n bytes at any alignment: 16-byte stores over the aligned interior
+__device__ void zero_bytes(uint8_t *p, u32 n)
+{
+    const uint4 z = make_uint4(0u, 0u, 0u, 0u);
+    const u32 head = (u32)((16u - ((uintptr_t)p & 15u)) & 15u);
+    const u32 h = head < n ? head : n;
+    st_range16(p + h - 16, z, 16u - h, 16u);
+    u32 o = h;
+    for (; o + 16u <= n; o += 16u)
+        *reinterpret_cast<uint4 *>(p + o) = z;
+    st_range16(p + o, z, 0u, n - o);
+}
+
+// Line staging for a wave of outputs at ANY byte offset (ragged segments, dense body
+// packing, bodies interleaved with wire headers).  MI355X writes a 128-byte line fast only
+// when one store instruction covers it whole (tools/diag: 4.5 TB/s against 2.8 TB/s for
+// lines written piecewise), so lines are ABSOLUTE: lane L's output [mine, mine + total)
+// starts d = mine & 127 bytes into its first line.  Its LDS row holds the line being built
+// (bytes [0, 128)) plus up to 64 bytes of the next; chunk q lands at (d + 64q) & 127 with
+// unaligned ds_write_b128, and completes a line when it reaches byte 128: at even q for
+// "class A" outputs (d >= 64), at odd q for the others.  The wave then stores that line of 8
+// outputs per global_store_dwordx4 (8 lanes x 16 bytes; each output's base and byte count
+// come from its owner lane by ds_bpermute) and each completing lane moves its row's bytes
+// [128, 192) to the front.  A wave whose lanes are all of one class (the kernels sort lanes
+// by class, class_permute) flushes once per chunk pair like EmitLines; a mixed wave flushes
+// at every chunk with the other class masked off.  Units that an output only partly covers
+// -- its first and last, the tag slot -- are clipped to its bytes (st_range16): neighbouring
+// outputs own the other bytes.  emit/finish/close must be reached by all 64 lanes together:
+// ds_bpermute from an inactive lane returns garbage, not its base.
+constexpr u32 SROW = 208;  // 192 bytes used; 52 dwords apart: conflict-free 16-lane b128
+constexpr u32 SHIFT_LDS_BYTES = 64 * SROW;  // EmitShiftLines: 13 KiB per wave
+struct EmitShiftLines {
+    static constexpr bool cooperative = true;
+    uint8_t *rows;   // this wave's 64 rows of SROW bytes
+    uint8_t *mine;
+    u32 lane, total, last_q;
+    u32 te;          // end of the output in its line space, d + total | bit 31: leave output bytes 16..31 to tag()
+    u32 mixed;       // the wave holds outputs of both classes
+
+    // the launchers keep d + total below 2^31
+    __device__ __forceinline__ void init(bool tag_slot)
+    {
+        te = (((u32)(uintptr_t)mine & 127u) + total) | (tag_slot ? 0x80000000u : 0u);
+        const uint64_t a = __builtin_amdgcn_ballot_w64((((u32)(uintptr_t)mine) & 64u) != 0u);
+        mixed = (a != 0 && ~a != 0) ? 1u : 0u;
+    }
+    // store, for every output F of the wave whose line completes now, its line k_F:
+    // KIND FL_PHASE: a one-class wave after chunk q of its phase, every F's line k = q / 2;
+    // KIND FL_MIXED: after chunk q, k_F = (d_F + 64q) / 128 for the F with bit 6 of d_F + 64q set;
+    // KIND FL_FINAL: after the last chunk q, the line holding output bytes past chunk q's line.
+    enum { FL_PHASE = 0, FL_MIXED = 1, FL_FINAL = 2 };
+    template <int KIND>
+    __device__ __forceinline__ void flush(u32 q)
+    {
+        const u32 c = lane & 7u;
+        const u32 r = lane >> 3;
+        const u64 mb = (u64)(uintptr_t)mine;
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // the other lanes' ds_writes of this line
+#pragma unroll
+        for (u32 j = 0; j < 8; j++) {
+            const u32 F = 8u * j + r;
+            const uint4 v = *reinterpret_cast<const uint4 *>(rows + F * SROW + 16u * c);
+            const int sel = (int)(F << 2);
+            const u32 blo = (u32)__builtin_amdgcn_ds_bpermute(sel, (int)(u32)mb);
+            const u32 bhi = (u32)__builtin_amdgcn_ds_bpermute(sel, (int)(u32)(mb >> 32));
+            const u32 fe = (u32)__builtin_amdgcn_ds_bpermute(sel, (int)te);
+            const u32 d = blo & 127u;           // output F's bytes are [d, e) of its line space
+            const u32 e = fe & 0x7fffffffu;
+            u32 k;
+            bool act = true;
+            if constexpr (KIND == FL_PHASE) {
+                k = q >> 1;
+            } else if constexpr (KIND == FL_MIXED) {
+                const u32 t = d + 64u * q;
+                k = t >> 7;
+                act = (t & 64u) != 0u;
+            } else {
+                k = (d + 64u * (q + 1u)) >> 7;
+                act = e > 128u * k;
+            }
+            const u32 u = 128u * k + 16u * c;  // this lane's unit of line k
+            const u64 p = ((((u64)bhi) << 32) | (blo & ~127u)) + u;
+            // overlaps the tag slot, output bytes 16..31: u + 16 > d + 16 && u < d + 32 (lines 0 and 1 only)
+            const bool tg = (KIND != FL_PHASE || q < 4u) && (fe >> 31) && u > d && u < d + 32u;
+            if (act && u >= d && u + 16u <= e && !tg) {
+                *reinterpret_cast<g_uint4 *>(p) = v4u_t{v.x, v.y, v.z, v.w};
+            } else if (act && u < e && u + 16u > d) {
+                // tag bytes [d + 16 - u, d + 32 - u) of this unit stay for tag()
+                st_unit_clip(p, v, d > u ? d - u : 0u, e < u + 16u ? e - u : 16u,
+                             tg ? (u < d + 16u ? d + 16u - u : 0u) : 0u,
+                             tg ? (d + 32u - u < 16u ? d + 32u - u : 16u) : 0u);
+            }
+        }
+    }
+    // a lane whose line just left keeps the bytes it already holds past it, end - 128 of them,
+    // for the next line (LDS ops of one wave execute in order: the flush's reads come first)
+    __device__ __forceinline__ void shift_row(u32 end)
+    {
+        asm volatile("" ::: "memory");
+        uint4 *row = reinterpret_cast<uint4 *>(rows + lane * SROW);
+#pragma unroll
+        for (u32 u = 0; u < 4; u++)
+            if (128u + 16u * u < end)
+                row[u] = row[8u + u];
+        asm volatile("" ::: "memory");
+    }
+    __device__ __forceinline__ void emit(u32 q, const u32 D[16])
+    {
+        const u32 t = ((u32)(uintptr_t)mine & 127u) + 64u * q;
+        const u32 pos = t & 127u;
+        uint8_t *w = rows + lane * SROW + pos;
+#pragma unroll
+        for (u32 c = 0; c < 4; c++)
+            reinterpret_cast<U16ua *>(w + 16u * c)->v = make_uint4(D[4 * c], D[4 * c + 1], D[4 * c + 2], D[4 * c + 3]);
+        const bool done = (t & 64u) != 0u;
+        if (mixed) {
+            flush<FL_MIXED>(q);
+        } else if (__builtin_amdgcn_readfirstlane(done ? 1u : 0u)) {
+            flush<FL_PHASE>(q);
+        } else {
+            last_q = q;
+            return;
+        }
+        if (__builtin_amdgcn_ballot_w64(done && pos + 64u > 128u) != 0 && done)
+            shift_row(pos + 64u);
+        last_q = q;
+    }
+    __device__ __forceinline__ void emit_full(u32 q, const u32 D[16]) { emit(q, D); }
+    __device__ __forceinline__ void tag(const u32 t[4])
+    {
+        reinterpret_cast<U16ua *>(mine + 16)->v = make_uint4(t[0], t[1], t[2], t[3]);
+    }
+    __device__ __forceinline__ void finish()
+    {
+        // bytes past an output are clipped by its count; the line after the last completed one
+        // still holds output bytes unless the output ends on it
+        const u32 t = ((u32)(uintptr_t)mine & 127u) + 64u * (last_q + 1u);
+        if (__builtin_amdgcn_ballot_w64(((u32)(uintptr_t)mine & 127u) + total > 128u * (t >> 7)) != 0)
+            flush<FL_FINAL>(last_q);
+    }
+    __device__ __forceinline__ void close(bool bad)
+    {
+        finish();
+        if (bad)
+            poison();
+    }
+    __device__ void poison()
+    {
+        __threadfence_block();  // land after the other lanes' stores of this lane's lines
+        zero_bytes(mine, total);
+    }
+};
+
 // Line staging for a wave of segments at arbitrary 16-byte aligned bases.  Like
 // EmitLines, 8 lanes write one 128-byte output line per store instruction, but
 // each frame's base and byte count are fetched from its owner lane with
@@ -984,7 +1252,9 @@ __device__ __forceinline__ u64 read_be64(const uint8_t *p)
 // stores are clipped to the segment's bytes (ragged frames are packed, nothing
 // is padding).  emit/finish/close must be reached by all 64 lanes together:
 // ds_bpermute from an inactive lane returns garbage, not its base.
+constexpr u32 SEG_LDS_BYTES = LINE_LDS_BYTES;  // EmitSegLines: 64 x 128-byte line buffer per wave
 struct EmitSegLines {
+    static constexpr bool cooperative = true;
     uint4 *lds;      // this wave's 64 x 8 chunks
     uint8_t *mine;
     u32 lane, total, last_q;
@@ -1056,6 +1326,36 @@ struct EmitSegLines {
     }
 };
 
+// Reorder the work items of one full workgroup so that each wave holds outputs of one
+// EmitShiftLines class (bit 6 of the output address): such a wave flushes once per chunk pair
+// instead of at every chunk.  `cls` is the class of this thread's own item; returns the
+// workgroup-relative index of the item this thread takes instead.  Deterministic (a
+// stable partition), so kernels that split waves between them agree on the layout.
+__device__ __forceinline__ u32 class_permute(bool cls)
+{
+    __shared__ u32 perm[BLOCK + WAVES];
+    const u32 tid = threadIdx.x, w = tid >> 6;
+    const uint64_t m = __builtin_amdgcn_ballot_w64(cls);
+    const u32 below1 = __builtin_amdgcn_mbcnt_hi((u32)(m >> 32), __builtin_amdgcn_mbcnt_lo((u32)m, 0u));
+    const u32 below0 = (tid & 63u) - below1;
+    if ((tid & 63u) == 0)
+        perm[BLOCK + w] = (u32)__builtin_popcountll(m);
+    __syncthreads();
+    u32 pre1 = 0, tot1 = 0;
+#pragma unroll
+    for (u32 i = 0; i < (u32)WAVES; i++) {
+        const u32 v = perm[BLOCK + i];
+        tot1 += v;
+        pre1 += i < w ? v : 0u;
+    }
+    const u32 pos = cls ? (BLOCK - tot1) + pre1 + below1 : (64u * w - pre1) + below0;
+    perm[pos] = tid;
+    __syncthreads();
+    const u32 mine = perm[tid];
+    __syncthreads();
+    return mine;
+}
+
 // Bytes of box blocks [b0, bend) that go to the output of a seal segment.
 __device__ __forceinline__ u32 seal_seg_bytes(u32 mlen, u32 b0, u32 bend)
 {
@@ -1072,7 +1372,7 @@ __device__ __forceinline__ u32 seal_seg_bytes(u32 mlen, u32 b0, u32 bend)
 // line's last 9 dwords.  Lane-wise 16-byte loads one block apart made L2 fetch
 // most lines twice (2.6x the payload on the Zipf batch).
 template <bool AL, class EM, bool PAIR = false>
-__device__ void seal_segment(const uint8_t *__restrict__ in, u32 n, u32 flags, u64 counter, const u32 key[8], u32 b0,
+__device__ __forceinline__ void seal_segment(const uint8_t *__restrict__ in, u32 n, u32 flags, u64 counter, const u32 key[8], u32 b0,
                              u32 b1, u32 *__restrict__ rec, EM &em, u32 nrun = 0)
 {
     const u32 mlen = n + 33u;
@@ -1271,7 +1571,7 @@ __device__ __forceinline__ OpenSeg open_seg_geom(u32 size, u32 b0, u32 b1)
 // Open box blocks [b0, b1) of one MESSAGE body whose header passed open_header.
 // Returns CZ_STATUS_OK or (whole frame, bad tag) CZ_STATUS_CRYPTO.
 template <bool AL, class EM>
-__device__ u32 open_segment(const uint8_t *__restrict__ in, u32 size, const u32 key[8], u32 n0, u32 n1, u32 b0,
+__device__ __forceinline__ u32 open_segment(const uint8_t *__restrict__ in, u32 size, const u32 key[8], u32 n0, u32 n1, u32 b0,
                             u32 b1, u32 *__restrict__ rec, u32 &flags_out, EM &em)
 {
     const OpenSeg g = open_seg_geom(size, b0, b1);
@@ -1412,7 +1712,7 @@ __device__ __forceinline__ void combine_tag(const u32 *__restrict__ R0, u32 nseg
 
 // ---- kernels -------------------------------------------------------------
 
-enum Staging { ST_DIRECT = 0, ST_LINES = 1, ST_REGION = 2 };
+enum Staging { ST_DIRECT = 0, ST_LINES = 1, ST_REGION = 2, ST_SHIFT = 3 };
 
 // Uniform batch of one connection direction: frame i = in[i*in_stride .. +len)
 // -> slot out[i*out_stride .. +out_stride), nonce counter0 + i, flags8[i] (or 0).
@@ -1426,8 +1726,17 @@ __global__ __launch_bounds__(BLOCK) CZ_OCC void k_seal_uniform(const uint8_t *__
                                                          const uint8_t *__restrict__ flags8, int allow_un0)
 {
     extern __shared__ uint4 smem[];
-    const uint32_t i = blockIdx.x * BLOCK + threadIdx.x;
-    const uint32_t wave_first = i & ~63u;
+    uint32_t i = blockIdx.x * BLOCK + threadIdx.x;
+    if constexpr (ST == ST_SHIFT) {
+        // waves of one line phase (EmitShiftLines): a full workgroup's frames sorted by class
+#ifndef CZ_XP_NO_PERMUTE
+        if (blockIdx.x * BLOCK + BLOCK <= count)
+#else
+        if (false)
+#endif
+            i = blockIdx.x * BLOCK + class_permute(((uintptr_t)(out + (uint64_t)i * out_stride) & 64u) != 0);
+    }
+    const uint32_t wave_first = (blockIdx.x * BLOCK + threadIdx.x) & ~63u;
     if (wave_first >= count)
         return;
     u32 key[8];
@@ -1449,6 +1758,15 @@ __global__ __launch_bounds__(BLOCK) CZ_OCC void k_seal_uniform(const uint8_t *__
                 seal_frame<MODE_ZMQ, true, EmitLines, PAIR, true>(src, len, fl, counter0 + i, key, em);
             else
                 seal_frame<MODE_ZMQ, true, EmitLines, PAIR, false>(src, len, fl, counter0 + i, key, em);
+        } else if constexpr (ST == ST_SHIFT) {
+            // bodies at any byte offset (dense packing, wire layout): byte-shifted line staging
+            EmitShiftLines em{reinterpret_cast<uint8_t *>(smem) + (threadIdx.x >> 6) * SHIFT_LDS_BYTES, dst, lane,
+                              mlen, 0u, 0u};
+            em.init(true);
+            if (un0)
+                seal_frame<MODE_ZMQ, true, EmitShiftLines, PAIR, true>(src, len, fl, counter0 + i, key, em);
+            else
+                seal_frame<MODE_ZMQ, true, EmitShiftLines, PAIR, false>(src, len, fl, counter0 + i, key, em);
         } else {
             const u32 st = (u32)out_stride;
             EmitRegion em{smem + (threadIdx.x >> 6) * ((64u * st) >> 4), out + (uint64_t)wave_first * out_stride, st,
@@ -1466,6 +1784,9 @@ __global__ __launch_bounds__(BLOCK) CZ_OCC void k_seal_uniform(const uint8_t *__
     if (aligned16(src, dst)) {
         EmitDirect<true> em{dst, mlen};
         seal_frame<MODE_ZMQ, true, EmitDirect<true>, PAIR>(src, len, fl, counter0 + i, key, em);
+    } else if ((((uintptr_t)src) & 15u) == 0) {
+        EmitDirect<false> em{dst, mlen};
+        seal_frame<MODE_ZMQ, true, EmitDirect<false>, PAIR>(src, len, fl, counter0 + i, key, em);
     } else {
         EmitDirect<false> em{dst, mlen};
         seal_frame<MODE_ZMQ, false>(src, len, fl, counter0 + i, key, em);
@@ -1600,7 +1921,6 @@ __global__ __launch_bounds__(BLOCK) CZ_OCC void k_open_uniform(const uint8_t *__
 
 
 // ---- segmented (ragged) batches ------------------------------------------
-constexpr u32 SEG_LDS_BYTES = LINE_LDS_BYTES;  // 64 x 128-byte line buffer per wave
 constexpr int SEGMODE_LINES = 1;  // line-staged stores for waves of equal-length segments
 constexpr int SEGMODE_PAIR = 2;   // whole-line input loads (seal)
 
@@ -1648,9 +1968,9 @@ __device__ __forceinline__ void seal_segments_body(const cz_frame_desc *__restri
 {
     const uint32_t t = blockIdx.x * BLOCK + threadIdx.x;
     const uint32_t wave_first = t & ~63u;
+    const bool allow_lines = mode & SEGMODE_LINES, pair = mode & SEGMODE_PAIR;
     if (wave_first >= nseg)
         return;
-    const bool allow_lines = mode & SEGMODE_LINES, pair = mode & SEGMODE_PAIR;
     const bool live = t < nseg;
     const cz_segment sg = segs[live ? t : wave_first];
     const cz_frame_desc d = desc[sg.frame];
@@ -1663,8 +1983,11 @@ __device__ __forceinline__ void seal_segments_body(const cz_frame_desc *__restri
     const u32 nch = (b1 < nblk ? b1 : nblk) - sg.first_block;
     const u32 total = seal_seg_bytes(mlen, sg.first_block, b1 < nblk ? b1 : nblk);
     const bool al = aligned16(src, dst);
+    // whole-line loads: a full wave of 16-byte aligned inputs takes a line emitter, EmitSegLines
+    // when every output is 16-byte aligned too, EmitShiftLines (any byte offset) otherwise
+    const bool in_al = (((uintptr_t)src) & 15u) == 0;
     const bool full_wave = wave_first + 64u <= nseg;
-    const bool lines = allow_lines && (pair ? wave_lines_ragged_ok(full_wave, al) : wave_lines_ok(full_wave, nch, al));
+    const bool lines = allow_lines && (pair ? wave_lines_ragged_ok(full_wave, in_al) : wave_lines_ok(full_wave, nch, al));
     if constexpr (PART == SEGPART_LINES) {
         if (!lines)
             return;
@@ -1678,14 +2001,24 @@ __device__ __forceinline__ void seal_segments_body(const cz_frame_desc *__restri
     if constexpr (PART != SEGPART_REST) {
         if (lines) {
             const u32 lane = threadIdx.x & 63u;
-            uint8_t *wl = reinterpret_cast<uint8_t *>(smem) + (threadIdx.x >> 6) * SEG_LDS_BYTES;
-            EmitSegLines em{reinterpret_cast<uint4 *>(wl), dst, lane, total, 0u, 0u};
-            em.init(sg.first_block == 0);
-            if (PART == SEGPART_LINES || pair)
-                seal_segment<true, EmitSegLines, true>(src, d.len, d.flags & 0xffu, d.counter, key, sg.first_block,
-                                                       b1, rec, em, wave_max(nch));
-            else
+            uint8_t *wl = reinterpret_cast<uint8_t *>(smem) + (threadIdx.x >> 6) * SHIFT_LDS_BYTES;
+            if (PART == SEGPART_LINES || pair) {
+                if (__builtin_amdgcn_ballot_w64(!al) == 0) {
+                    EmitSegLines em{reinterpret_cast<uint4 *>(wl), dst, lane, total, 0u, 0u};
+                    em.init(sg.first_block == 0);
+                    seal_segment<true, EmitSegLines, true>(src, d.len, d.flags & 0xffu, d.counter, key,
+                                                           sg.first_block, b1, rec, em, wave_max(nch));
+                } else {
+                    EmitShiftLines em{wl, dst, lane, total, 0u, 0u};
+                    em.init(sg.first_block == 0);
+                    seal_segment<true, EmitShiftLines, true>(src, d.len, d.flags & 0xffu, d.counter, key,
+                                                             sg.first_block, b1, rec, em, wave_max(nch));
+                }
+            } else {
+                EmitSegLines em{reinterpret_cast<uint4 *>(wl), dst, lane, total, 0u, 0u};
+                em.init(sg.first_block == 0);
                 seal_segment<true>(src, d.len, d.flags & 0xffu, d.counter, key, sg.first_block, b1, rec, em);
+            }
             return;
         }
     }
@@ -1756,7 +2089,7 @@ __global__ __launch_bounds__(BLOCK) void k_open_segments(const cz_frame_desc *__
 {
     const bool allow_lines = mode & SEGMODE_LINES;
     extern __shared__ uint4 smem[];
-    const uint32_t t = blockIdx.x * BLOCK + threadIdx.x;
+    uint32_t t = blockIdx.x * BLOCK + threadIdx.x;
     const uint32_t wave_first = t & ~63u;
     if (wave_first >= nseg)
         return;
@@ -1793,14 +2126,22 @@ __global__ __launch_bounds__(BLOCK) void k_open_segments(const cz_frame_desc *__
     uint8_t *dst = out + d.out_off + 64ull * g.cb;
     const u32 total = early == CZ_STATUS_OK ? (g.bend == g.nblk ? g.nout : 64u * g.ce) - 64u * g.cb : 0u;
     const bool al = aligned16(src, dst);
+    const bool in_al = (((uintptr_t)src) & 15u) == 0;  // the line emitter takes outputs at any byte offset
     u32 fl = 0;
-    if (allow_lines && wave_lines_ok(wave_first + 64u <= nseg, nch, al) &&
+    if (allow_lines && wave_lines_ok(wave_first + 64u <= nseg, nch, in_al) &&
         __builtin_amdgcn_ballot_w64(early != CZ_STATUS_OK) == 0) {
         const u32 lane = threadIdx.x & 63u;
-        uint8_t *wl = reinterpret_cast<uint8_t *>(smem) + (threadIdx.x >> 6) * SEG_LDS_BYTES;
-        EmitSegLines em{reinterpret_cast<uint4 *>(wl), dst, lane, total, 0u, 0u};
-        em.init(false);
-        const u32 st = open_segment<true>(src, d.len, key, n0, n1, sg.first_block, b1, rec, fl, em);
+        uint8_t *wl = reinterpret_cast<uint8_t *>(smem) + (threadIdx.x >> 6) * SHIFT_LDS_BYTES;
+        u32 st;
+        if (__builtin_amdgcn_ballot_w64(!al) == 0) {
+            EmitSegLines em{reinterpret_cast<uint4 *>(wl), dst, lane, total, 0u, 0u};
+            em.init(false);
+            st = open_segment<true>(src, d.len, key, n0, n1, sg.first_block, b1, rec, fl, em);
+        } else {  // plaintext at any byte offset
+            EmitShiftLines em{wl, dst, lane, total, 0u, 0u};
+            em.init(false);
+            st = open_segment<true>(src, d.len, key, n0, n1, sg.first_block, b1, rec, fl, em);
+        }
         if (!rec)
             status[sg.frame] = (uint16_t)(st | (st == CZ_STATUS_OK ? (fl << 8) : 0u));
         return;
@@ -2037,6 +2378,7 @@ int pick_staging(uint64_t stride, uint32_t out_bytes, bool aligned)
 static int g_pair = 1;
 static int g_un0 = 1;  // scalar first Salsa round when the high nonce word is wave-uniform
 static int g_seglines = 1;  // line-staged stores for waves of equal-length segments
+static int g_shift = 1;     // uniform seal: shifted line staging for bodies at any byte offset
 
 // ---------------------------------------------------------------------------
 // Launchers (called from cz_host.cpp).  No allocation, no synchronisation:
@@ -2051,21 +2393,28 @@ hipError_t czk_seal_uniform(const void *in, uint64_t in_stride, void *out, uint6
     if (count == 0)
         return hipSuccess;
     dim3 grid((count + BLOCK - 1) / BLOCK);
-    const bool al = ((((uintptr_t)in | (uintptr_t)out | in_stride | out_stride) & 15u) == 0);
+    const bool in_al = ((((uintptr_t)in | in_stride) & 15u) == 0);
+    const bool al = in_al && ((((uintptr_t)out | out_stride) & 15u) == 0);
 #define CZ_SEAL_LAUNCH(ST, PR, LDS)                                                                        \
     hipLaunchKernelGGL((k_seal_uniform<ST, PR>), grid, dim3(BLOCK), (LDS), s, (const uint8_t *)in, in_stride,   \
                        (uint8_t *)out, out_stride, count, len, (const uint8_t *)subkey, counter0, flags8, g_un0)
-    const int st = pick_staging(out_stride, len + 33u, al);
+    int st = pick_staging(out_stride, len + 33u, al);
+    // bodies at any byte offset (dense slots, wire layout) from aligned payloads: shifted line staging
+    if (st == ST_DIRECT && in_al && len + 33u >= 256u && len < 0x7fffff00u && g_shift)
+        st = ST_SHIFT;
     const unsigned lds = st == ST_LINES ? WAVES * (LINE_LDS_BYTES + HOLD_LDS_BYTES)
+                                        : st == ST_SHIFT ? WAVES * SHIFT_LDS_BYTES
                                         : (st == ST_REGION ? (unsigned)(WAVES * 64 * out_stride) : 0u);
     // whole-line input pays for large frames (A/B: 4 KiB seal 2.34 vs 2.51 ms) but
     // not for the small frames of the region stager (100 B: 0.119 vs 0.114 ms)
     if (g_pair && st != ST_REGION) {
         if (st == ST_LINES) CZ_SEAL_LAUNCH(ST_LINES, true, lds);
+        else if (st == ST_SHIFT) CZ_SEAL_LAUNCH(ST_SHIFT, true, lds);
         else CZ_SEAL_LAUNCH(ST_DIRECT, true, 0);
     } else {
         if (st == ST_LINES) CZ_SEAL_LAUNCH(ST_LINES, false, lds);
         else if (st == ST_REGION) CZ_SEAL_LAUNCH(ST_REGION, false, lds);
+        else if (st == ST_SHIFT) CZ_SEAL_LAUNCH(ST_SHIFT, false, lds);
         else CZ_SEAL_LAUNCH(ST_DIRECT, false, 0);
     }
 #undef CZ_SEAL_LAUNCH
@@ -2152,12 +2501,12 @@ hipError_t czk_seal_segments(const cz_frame_desc *desc, const cz_segment *segs, 
     if (nseg && g_seglines && g_pair) {
 #endif
         const int mode = SEGMODE_LINES | SEGMODE_PAIR;
-        hipLaunchKernelGGL(k_seal_segments_lines, grid, dim3(BLOCK), WAVES * SEG_LDS_BYTES, s, desc, segs, nseg,
+        hipLaunchKernelGGL(k_seal_segments_lines, grid, dim3(BLOCK), WAVES * SHIFT_LDS_BYTES, s, desc, segs, nseg,
                            (const uint8_t *)in, (uint8_t *)out, (const uint8_t *)subkeys, (u32 *)work, mode);
         hipLaunchKernelGGL(k_seal_segments, grid, dim3(BLOCK), 0, s, desc, segs, nseg, (const uint8_t *)in,
                            (uint8_t *)out, (const uint8_t *)subkeys, (u32 *)work, mode | SEGMODE_REST);
     } else if (nseg) {
-        hipLaunchKernelGGL(k_seal_segments, grid, dim3(BLOCK), WAVES * SEG_LDS_BYTES, s, desc, segs, nseg,
+        hipLaunchKernelGGL(k_seal_segments, grid, dim3(BLOCK), WAVES * SHIFT_LDS_BYTES, s, desc, segs, nseg,
                            (const uint8_t *)in, (uint8_t *)out, (const uint8_t *)subkeys, (u32 *)work,
                            (g_seglines ? SEGMODE_LINES : 0) | (g_pair ? SEGMODE_PAIR : 0));
     }
@@ -2172,7 +2521,7 @@ hipError_t czk_open_segments(const cz_frame_desc *desc, const cz_segment *segs, 
                              uint16_t *status, uint64_t *nonces, hipStream_t s)
 {
     if (nseg)
-        hipLaunchKernelGGL(k_open_segments, dim3((nseg + BLOCK - 1) / BLOCK), dim3(BLOCK), WAVES * SEG_LDS_BYTES, s,
+        hipLaunchKernelGGL(k_open_segments, dim3((nseg + BLOCK - 1) / BLOCK), dim3(BLOCK), WAVES * SHIFT_LDS_BYTES, s,
                            desc, segs, nseg, (const uint8_t *)in, (uint8_t *)out, (const uint8_t *)subkeys,
                            (u32 *)work, status, nonces, (g_seglines ? SEGMODE_LINES : 0) | (g_pair ? SEGMODE_PAIR : 0));
     if (ncomb)
@@ -2208,6 +2557,11 @@ int czk_tune(const char *key, int value)
     if (__builtin_strcmp(key, "seglines") == 0) {
         int old = g_seglines;
         g_seglines = value != 0;
+        return old;
+    }
+    if (__builtin_strcmp(key, "shift") == 0) {
+        int old = g_shift;
+        g_shift = value != 0;
         return old;
     }
     return -1;

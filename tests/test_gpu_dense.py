@@ -1,0 +1,159 @@
+"""GPU parity for bodies at ANY byte offset: the shifted line emitter (EmitSegLines).
+
+Dense output is what the wire needs (bodies back to back, or behind V2 headers,
+V2Encoder.java:23-56): a 4 KiB body slot of 4129 bytes puts every frame at a
+different byte phase of the 128-byte line.  Cases:
+  * cz_seal_uniform at strides 4129 (dense), 4130, 4131, 4136, 4144 and 4226, at output
+    bases shifted by 0..15 bytes, with a partial last wave: every body bit-exact against
+    the oracle (CurveClientMechanism.encode -> Curve.afternm, Curve.java:129-137), and
+    every byte between bodies left as the caller wrote it;
+  * cz_seal_segments with ragged frames packed densely (byte offsets) and on the 8-byte
+    offset table of SURVEY.md 8(d) row 4, short and long segments;
+  * cz_open_segments writing plaintext densely (CurveClientMechanism.decode).
+"""
+import numpy as np
+import pytest
+
+from cz_testlib import DESC_DTYPE, load_golden, oracle, oracle_check_full, or_curve_encode, splitmix_bytes
+
+pytestmark = pytest.mark.gpu
+
+G = load_golden()
+PRECOM = bytes.fromhex(G["keys"]["precom"])
+SENTINEL = 0xA5
+
+
+@pytest.fixture(scope="module")
+def torch_dev():
+    import torch
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    return torch, torch.device("cuda:0")
+
+
+@pytest.fixture(scope="module")
+def subkeys(torch_dev):
+    torch, dev = torch_dev
+    from jeromq_amd import _lib, batch
+    k = torch.tensor(list(PRECOM), dtype=torch.uint8, device=dev).view(1, 32)
+    return torch.cat([batch.subkeys(k, _lib.CZ_DIR_C2S), batch.subkeys(k, _lib.CZ_DIR_S2C)])
+
+
+def _gaps_untouched(out, spans, lo, hi):
+    """bytes of out[lo:hi] outside every [s, e) span still hold the sentinel"""
+    mask = np.ones(hi - lo, dtype=bool)
+    for s, e in spans:
+        mask[s - lo:e - lo] = False
+    bad = np.nonzero(out[lo:hi][mask] != SENTINEL)[0]
+    assert bad.size == 0, f"{bad.size} bytes outside the bodies were written (first at {lo + int(np.nonzero(mask)[0][bad[0]])})"
+
+
+@pytest.mark.parametrize("n,stride", [(4096, 4129), (4096, 4130), (4096, 4131), (4096, 4136), (4096, 4144),
+                                      (4096, 4226), (223, 256 + 5), (300, 333), (1000, 1041)])
+@pytest.mark.parametrize("base", [0, 1, 8, 13])
+def test_seal_uniform_any_offset(torch_dev, subkeys, n, stride, base):
+    torch, dev = torch_dev
+    from jeromq_amd import batch
+    count = 64 * 5 + 17  # five full waves and a partial one
+    in_stride = (n + 15) // 16 * 16
+    hin = np.frombuffer(splitmix_bytes(count * in_stride, 1000 + n + stride), dtype=np.uint8).copy()
+    d_in = torch.from_numpy(hin).to(dev)
+    size = base + count * stride + 64
+    d_buf = torch.full((size,), SENTINEL, dtype=torch.uint8, device=dev)
+    d_out = d_buf[base:]
+    flags = torch.tensor([(i % 3 == 0) | (2 if i % 5 == 0 else 0) for i in range(count)], dtype=torch.uint8, device=dev)
+    c0 = 0xFFFFFFF0 - 100  # the high nonce word changes inside a wave
+    batch.seal_uniform(d_in, in_stride, d_out, stride, count, n, subkeys[0], c0, flags8=flags)
+    torch.cuda.synchronize()
+    out = d_buf.cpu().numpy()
+    fl = flags.cpu().numpy()
+    spans = []
+    for i in range(count):
+        o = base + i * stride
+        want = or_curve_encode(hin[i * in_stride:i * in_stride + n].tobytes(), int(fl[i]), c0 + i, 0, PRECOM)
+        got = out[o:o + n + 33].tobytes()
+        assert got == want, f"frame {i} (stride {stride}, base {base}) differs from the oracle"
+        spans.append((o, o + n + 33))
+    _gaps_untouched(out, spans, 0, size)
+
+
+def _ragged(lens, out_round, in_align=64):
+    """payloads on in_align boundaries, bodies packed at out_round-byte granularity (1 = dense)"""
+    desc = np.zeros(len(lens), dtype=DESC_DTYPE)
+    io = oo = 0
+    for i, n in enumerate(lens):
+        desc[i] = (io, oo, n, 0, 3 + i, 1 if i % 8 == 0 else 0, -1)
+        io += (n + in_align - 1) // in_align * in_align
+        oo += (n + 33 + out_round - 1) // out_round * out_round
+    hin = np.zeros(io + 64, dtype=np.uint8)
+    for i, n in enumerate(lens):
+        o = int(desc[i]["in_off"])
+        hin[o:o + n] = np.frombuffer(splitmix_bytes(n, 5 + 31 * i), dtype=np.uint8)
+    return desc, hin, oo + 64
+
+
+def _zipf_lens(count, seed):
+    rng = np.random.default_rng(seed)
+    j = rng.zipf(1.2, size=4 * count)
+    j = j[j <= 1024][:count]
+    return [int(64 * x) for x in j]
+
+
+@pytest.mark.parametrize("out_round", [1, 8])
+@pytest.mark.parametrize("seg_blocks", [3, 64])
+def test_seal_segments_dense_outputs(torch_dev, subkeys, out_round, seg_blocks):
+    torch, dev = torch_dev
+    from jeromq_amd import batch
+    lens = _zipf_lens(3000, 42) + [0, 1, 31, 65536, 4096, 4095, 100, 223]
+    desc, hin, ob = _ragged(lens, out_round)
+    plan = batch.SegmentPlan(desc, open_=False, seg_blocks=seg_blocks).to(dev)
+    d_in = torch.from_numpy(hin).to(dev)
+    d_out = torch.full((ob,), SENTINEL, dtype=torch.uint8, device=dev)
+    d_desc = torch.from_numpy(desc.view(np.uint8).copy()).to(dev)
+    batch.seal_segments(d_desc, plan, d_in, d_out, subkeys, desc_np=desc)
+    torch.cuda.synchronize()
+    assert oracle_check_full(d_in, d_out, desc, PRECOM) == len(desc)
+    out = d_out.cpu().numpy()
+    spans = [(int(d["out_off"]), int(d["out_off"]) + int(d["len"]) + 33) for d in desc]
+    _gaps_untouched(out, spans, 0, ob)
+
+
+@pytest.mark.parametrize("out_round", [1, 8])
+def test_open_segments_dense_plaintext(torch_dev, subkeys, out_round):
+    """bodies on 16-byte boundaries, plaintext packed densely: every payload recovered, gaps kept"""
+    torch, dev = torch_dev
+    from jeromq_amd import batch
+    lens = _zipf_lens(2000, 7) + [0, 1, 65536, 4096]
+    count = len(lens)
+    desc = np.zeros(count, dtype=DESC_DTYPE)
+    bodies, io = [], 0
+    for i, n in enumerate(lens):
+        p = splitmix_bytes(n, 900 + i)
+        b = or_curve_encode(p, i & 1, 10 + i, 0, PRECOM)
+        bodies.append((io, p, b))
+        io += (len(b) + 15) // 16 * 16
+    hin = np.zeros(io + 64, dtype=np.uint8)
+    oo = 0
+    for i, (o, p, b) in enumerate(bodies):
+        hin[o:o + len(b)] = np.frombuffer(b, dtype=np.uint8)
+        # the server opens client bodies: nonce floor 9 for the first, chained through prev
+        desc[i] = (o, oo, len(b), 0, 9, 0, i - 1 if i else -1)
+        oo += (len(p) + out_round - 1) // out_round * out_round if p else out_round
+    desc["flags"] |= np.uint32(1 << 8)  # CZ_DESC_CHECK_NONCE
+    ob = oo + 64
+    plan = batch.SegmentPlan(desc, open_=True, seg_blocks=64).to(dev)
+    d_out = torch.full((ob,), SENTINEL, dtype=torch.uint8, device=dev)
+    status = torch.full((count,), -1, dtype=torch.int16, device=dev)
+    batch.open_segments(torch.from_numpy(desc.view(np.uint8).copy()).to(dev), plan, torch.from_numpy(hin).to(dev),
+                        d_out, subkeys, status, desc_np=desc)
+    torch.cuda.synchronize()
+    st = status.cpu().numpy().view(np.uint16)
+    out = d_out.cpu().numpy()
+    spans = []
+    for i, (o, p, b) in enumerate(bodies):
+        assert st[i] & 0xff == 0, f"frame {i}: status {st[i]:#x}"
+        assert (st[i] >> 8) == (i & 1)
+        s = int(desc[i]["out_off"])
+        assert out[s:s + len(p)].tobytes() == p, f"frame {i} (len {len(p)}) plaintext differs"
+        spans.append((s, s + len(p)))
+    _gaps_untouched(out, spans, 0, ob)

@@ -471,11 +471,17 @@ int cz_plan_segments(const cz_frame_desc *h_desc, uint32_t count, int open, uint
         const uint32_t ce = bend == nblk ? (len - CZ_MESSAGE_OVERHEAD + 63) / 64 : bend - 1;
         return ce - cb;
     };
-    std::vector<std::pair<uint32_t, uint32_t>> key(segs.size());
+    // Seal, within one length: segments whose input starts on a 128-byte line first, then the
+    // ones starting 64 bytes into a line, so that waves hold one line phase and the odd ones
+    // can read whole lines (seal_segment in cz_kernels.hip).  Key: chunks * 2 + (1 - phase).
+    auto phase = [&](const cz_segment &g) -> uint32_t {
+        return open ? 0u : (uint32_t)(((h_desc[g.frame].in_off + 64ull * g.first_block) >> 6) & 1u);
+    };
+    std::vector<std::pair<uint64_t, uint32_t>> key(segs.size());
     for (size_t k = 0; k < segs.size(); k++)
-        key[k] = {chunks(segs[k]), (uint32_t)k};
-    std::stable_sort(key.begin(), key.end(), [](const std::pair<uint32_t, uint32_t> &a,
-                                                 const std::pair<uint32_t, uint32_t> &b) { return a.first > b.first; });
+        key[k] = {2ull * chunks(segs[k]) + (1u - phase(segs[k])), (uint32_t)k};
+    std::stable_sort(key.begin(), key.end(), [](const std::pair<uint64_t, uint32_t> &a,
+                                                 const std::pair<uint64_t, uint32_t> &b) { return a.first > b.first; });
     std::vector<cz_segment> sorted(segs.size());
     for (size_t k = 0; k < segs.size(); k++)
         sorted[k] = segs[key[k].second];

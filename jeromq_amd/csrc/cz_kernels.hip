@@ -1426,8 +1426,37 @@ __device__ __forceinline__ void seal_segment(const uint8_t *__restrict__ in, u32
 
     if constexpr (PAIR) {
         static_assert(AL, "PAIR needs 16-byte aligned input");
-        u32 cy[9];  // P[16*b0 - 9 .. 16*b0 - 1]
-        if (b0 == 0) {
+        u32 cy[9];  // P[16*(b0+q0) - 9 .. 16*(b0+q0) - 1]
+        // nrun (cooperative emitters): the wave's longest segment; shorter ones run along
+        const u32 run = nrun > nch ? nrun : nch;
+        // Line phase.  Pair k reads payload [64(b0 + 2k), +128): a whole 128-byte line only when
+        // in + 64*b0 is line-aligned.  Otherwise ("odd", half of a 64-byte packed ragged batch)
+        // every pair load straddles two lines and each line is fetched twice, one pair apart
+        // (FETCH 1.47x the payload).  A wave whose segments are all odd (the planner sorts
+        // segments by phase within a length) seals block b0 alone from the line that ends
+        // 64 bytes into it, then pairs (b0+1, b0+2), ... from whole lines.
+        const bool odd = (((uintptr_t)(in + 64u * b0)) & 64u) != 0u;
+        u32 q0 = 0;
+        if (__builtin_amdgcn_ballot_w64(!odd) == 0) {
+            // line [64*b0 - 64, 64*b0 + 64): aligned, so on a mapped page even where it starts
+            // before the payload (bytes outside the frame are never used)
+            const uint8_t *ln = in + 64u * b0 - 64;
+            u32 L[32];
+#pragma unroll
+            for (int c = 0; c < 8; c++) {
+                const long o = (long)(64u * b0) - 64 + 16 * c;
+                V4 v = (o < 0) ? zero4() : ld16<AL>(ln + 16 * c, (u64)o < inlen ? inlen - (u64)o : 0);
+                L[4 * c] = v.x; L[4 * c + 1] = v.y; L[4 * c + 2] = v.z; L[4 * c + 3] = v.w;
+            }
+            if (b0 == 0)
+                L[15] = flags << 24;  // P[-1]
+            block(b0, L + 7, 0u < nch);
+            em.emit(0u, C);
+#pragma unroll
+            for (int k = 0; k < 9; k++)
+                cy[k] = L[23 + k];
+            q0 = 1;
+        } else if (b0 == 0) {
 #pragma unroll
             for (int k = 0; k < 8; k++)
                 cy[k] = 0u;
@@ -1438,9 +1467,7 @@ __device__ __forceinline__ void seal_segment(const uint8_t *__restrict__ in, u32
             cy[0] = a.w; cy[1] = b.x; cy[2] = b.y; cy[3] = b.z; cy[4] = b.w;
             cy[5] = c.x; cy[6] = c.y; cy[7] = c.z; cy[8] = c.w;
         }
-        // nrun (cooperative emitters): the wave's longest segment; shorter ones run along
-        const u32 run = nrun > nch ? nrun : nch;
-        for (u32 q = 0; q < run; q += 2u) {
+        for (u32 q = q0; q < run; q += 2u) {
             const u32 blk = b0 + q;
             const uint8_t *src = in + 64u * blk;
             const u64 o = 64ull * blk;

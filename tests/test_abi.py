@@ -103,3 +103,33 @@ def test_argument_validation(lib):
     assert lib.cz_seal_uniform(4, 100, None, 100, None, 133, None, 0, None, None) == _lib.CZ_EINVAL
     assert lib.cz_seal_uniform(4, 100, 16, 50, 16, 133, 16, 0, None, None) == _lib.CZ_EINVAL  # stride < len
     assert lib.cz_subkeys(16, 16, 1, 7, None) == _lib.CZ_EINVAL
+
+
+def test_plan_segments_orders_by_length_then_line_phase(lib):
+    """cz_plan_segments (host): longest first; within one length, segments whose input starts on
+    a 128-byte line before those starting 64 bytes into one (seal), so waves hold one phase."""
+    import numpy as np
+    from jeromq_amd.batch import DESC_DTYPE, SegmentPlan
+    rng = np.random.default_rng(3)
+    lens = (64 * rng.integers(1, 300, size=700)).astype(np.uint64)
+    d = np.zeros(len(lens), dtype=DESC_DTYPE)
+    d["len"] = lens
+    d["in_off"][1:] = np.cumsum(lens[:-1])  # 64-byte packing: both phases occur
+    plan = SegmentPlan(d, open_=False, seg_blocks=8)
+    seg = plan.segments
+    mlen = lens[seg["frame"]] + np.uint64(33)
+    nb = seg["nblocks"].astype(np.int64)
+    ph = ((d["in_off"][seg["frame"]] + np.uint64(64) * seg["first_block"].astype(np.uint64)) >> np.uint64(6)) & np.uint64(1)
+    key = 2 * nb + (1 - ph.astype(np.int64))
+    assert np.all(np.diff(key) <= 0)
+    # every box block of every frame covered exactly once
+    cover = {}
+    for s in seg:
+        cover.setdefault(int(s["frame"]), []).append((int(s["first_block"]), int(s["nblocks"])))
+    for f, parts in cover.items():
+        parts.sort()
+        nblk = (int(lens[f]) + 33 + 63) // 64
+        assert parts[0][0] == 0 and sum(n for _, n in parts) == nblk
+        for (a, n), (b, _) in zip(parts, parts[1:]):
+            assert a + n == b
+    assert len(cover) == len(lens) and int(mlen.min()) >= 97

@@ -49,7 +49,7 @@ def parse():
                     help="zipf: input payload slot alignment in bytes (lengths are 64-byte multiples)")
     ap.add_argument("--out-align", type=int, default=128,
                     help="zipf: output slot alignment in bytes (the caller's packing choice)")
-    ap.add_argument("--config", default="4k", choices=["4k", "4k_dense", "100b", "zipf", "zipf_lane", "open4k", "e2e4k", "engine",
+    ap.add_argument("--config", default="4k", choices=["4k", "4k_dense", "100b", "zipf", "zipf_lane", "open4k", "e2e4k", "engine", "nacl",
                                                           "beforenm"])
     ap.add_argument("--frames", type=int, default=FRAMES)
     ap.add_argument("--no-cpu-baseline", action="store_true")
@@ -275,6 +275,53 @@ def cpu_baseline(wl, target_s):
                       f"{os.cpu_count()} logical CPUs visible"}
 
 
+def copy_ceiling(dev, nbytes=1 << 30, chunk=64 << 20, reps=5):
+    """PCIe copy ceilings the host-resident lines sit under: pinned H2D alone, D2H alone, and both
+    at once (full duplex), nbytes per direction in `chunk`-byte hipMemcpyAsync calls, each
+    direction on its own stream (as the 3-stream pipelines issue them).  Median GB/s."""
+    hip = ctypes.CDLL("libamdhip64.so")
+    vp, sz = ctypes.c_void_p, ctypes.c_size_t
+    hip.hipMemcpyAsync.argtypes = [vp, vp, sz, ctypes.c_int, vp]
+    hip.hipStreamSynchronize.argtypes = [vp]
+    hip.hipHostFree.argtypes = [vp]
+    hip.hipFree.argtypes = [vp]
+    hip.hipSetDevice(dev.index or 0)
+    bufs = [vp() for _ in range(4)]
+    for b in bufs[:2]:
+        assert hip.hipHostMalloc(ctypes.byref(b), sz(nbytes), 0) == 0, "hipHostMalloc"
+    for b in bufs[2:]:
+        assert hip.hipMalloc(ctypes.byref(b), sz(nbytes)) == 0, "hipMalloc"
+    h_src, h_dst, d_a, d_b = (b.value for b in bufs)
+    sa, sb = vp(), vp()
+    hip.hipStreamCreateWithFlags(ctypes.byref(sa), 1)
+    hip.hipStreamCreateWithFlags(ctypes.byref(sb), 1)
+
+    def timed(h2d, d2h):
+        ts = []
+        for _ in range(reps + 1):
+            t0 = time.perf_counter()
+            for off in range(0, nbytes, chunk):
+                if h2d:
+                    assert hip.hipMemcpyAsync(d_a + off, h_src + off, chunk, 1, sa) == 0
+                if d2h:
+                    assert hip.hipMemcpyAsync(h_dst + off, d_b + off, chunk, 2, sb) == 0
+            hip.hipStreamSynchronize(sa)
+            hip.hipStreamSynchronize(sb)
+            ts.append(time.perf_counter() - t0)
+        return float(np.median(ts[1:]))
+    t_h, t_d, t_b = timed(True, False), timed(False, True), timed(True, True)
+    hip.hipStreamDestroy(sa)
+    hip.hipStreamDestroy(sb)
+    for b in bufs[:2]:
+        hip.hipHostFree(b)
+    for b in bufs[2:]:
+        hip.hipFree(b)
+    return {"h2d_GBps": round(nbytes / t_h / 1e9, 2), "d2h_GBps": round(nbytes / t_d / 1e9, 2),
+            "bidir_GBps_total": round(2 * nbytes / t_b / 1e9, 2), "bytes_per_direction": nbytes,
+            "method": f"hipMemcpyAsync of pinned buffers in {chunk >> 20} MiB calls, one stream per direction, "
+                      f"median of {reps}"}
+
+
 def e2e_host(args, dev):
     """End-to-end from pinned host memory (the JNI path): H2D + seal + D2H pipelined over 3
     streams by cz_ctx_seal_uniform, then the reverse open.  Wall clock, payload GiB/s."""
@@ -322,10 +369,13 @@ def e2e_host(args, dev):
     for p in (pin, pout, pback, pstat):
         lib.cz_host_free(p)
     pay = frames * n
+    ceil = copy_ceiling(dev)
+    pcie = frames * (in_stride + out_stride) / res["seal"] / 1e9
     return {"metric": "CURVE seal GiB/s end-to-end from pinned host memory (H2D + seal + D2H), 4 KiB frames",
             "value": round(pay / res["seal"] / 2**30, 3), "unit": "GiB/s", "n_gpus": 1,
             "open_GiBps": round(pay / res["open"] / 2**30, 3),
-            "pcie_bytes_per_s": round((frames * (in_stride + out_stride)) / res["seal"] / 1e9, 2),
+            "pcie_bytes_per_s": round(pcie, 2),
+            "copy_ceiling": ceil, "frac_of_bidir_ceiling": round(pcie / ceil["bidir_GBps_total"], 3),
             "config": {"workload": f"{frames} x 4 KiB frames, pinned host buffers, 3-stream pipeline, "
                                    f"{chunk}-frame chunks", "frames": frames}}
 
@@ -375,12 +425,105 @@ def engine_host(args, dev):
     ok = ok and len(got) == per and got[-1][0] == payload[(per - 1) * n:per * n]
     ok = ok and all(srv.error(sc[c])[0] == 0 for c in range(nconn))
     msgs = nconn * per
+    ceil = copy_ceiling(dev)
+    wire_bytes = sum(len(x) for x in wires)
     return {"metric": "CURVE batching engine end-to-end GiB/s (pinned host, 1024 connections, ZMTP v2 wire)",
+            "copy_ceiling": ceil,
+            "flush_out_pcie_GBps": round((total + wire_bytes) / res["flush_out_s"] / 1e9, 2),
             "value": round(total / res["flush_out_s"] / 2**30, 3), "unit": "GiB/s", "n_gpus": 1,
             "open_GiBps": round(total / res["flush_in_s"] / 2**30, 3),
             "msgs_per_s_out": round(msgs / res["flush_out_s"], 1), "msgs_per_s_in": round(msgs / res["flush_in_s"], 1),
             "timings_s": {k: round(v, 4) for k, v in res.items()}, "verified": bool(ok),
             "config": {"workload": f"{nconn} connections x {per} x {n} B MESSAGEs per flush", "frames": msgs}}
+
+
+def _libsodium():
+    """libsodium from the image (an optimised CPU NaCl, for comparison only; None if absent)."""
+    for path in ("/opt/conda/lib/libsodium.so", "libsodium.so.23", "libsodium.so"):
+        try:
+            L = ctypes.CDLL(path)
+            if L.sodium_init() >= 0:
+                return L
+        except OSError:
+            pass
+    return None
+
+
+def nacl_latency(args, dev):
+    """Single-message latency of the jnacl drop-ins (cz_box_afternm / cz_box_open_afternm, the
+    Curve.afternm / openAfternm path of INTEGRATION.md section 2: one message per call, host
+    buffers in and out), at 100 B / 4 KiB / 64 KiB, beside one CPU core (the oracle port and
+    libsodium), and the batch size at which the host-staged batched API (cz_ctx_seal_uniform)
+    beats one CPU core per message.  Wall clock through ctypes, median of many calls."""
+    lib = _lib.lib()
+    sys.path.insert(0, os.path.join(ROOT, "tests"))
+    from cz_testlib import oracle
+    orc = oracle()
+    sod = _libsodium()
+    k = (ctypes.c_uint8 * 32).from_buffer_copy(PRECOM)
+    nonce = (ctypes.c_uint8 * 24).from_buffer_copy(b"CurveZMQMESSAGEC" + (3).to_bytes(8, "big"))
+
+    def med(fn, reps, budget_s=1.5):
+        fn()
+        ts = []
+        t_end = time.perf_counter() + budget_s
+        for _ in range(reps):
+            t0 = time.perf_counter()
+            fn()
+            ts.append(time.perf_counter() - t0)
+            if time.perf_counter() > t_end and len(ts) >= 5:
+                break
+        return float(np.median(ts))
+    t_ctypes = med(lambda: lib.cz_version(), 2000)
+    rows = []
+    for n in (100, 4096, 65536):
+        mlen = n + 32
+        m = (ctypes.c_uint8 * mlen)()
+        m[32:] = list(np.random.default_rng(n).integers(0, 256, size=n, dtype=np.uint8))
+        c = (ctypes.c_uint8 * mlen)()
+        back = (ctypes.c_uint8 * mlen)()
+        t_seal = med(lambda: lib.cz_box_afternm(c, m, mlen, nonce, k), 400)
+        t_open = med(lambda: lib.cz_box_open_afternm(back, c, mlen, nonce, k), 400)
+        ok = lib.cz_box_afternm(c, m, mlen, nonce, k) == 0 and bytes(c) == orc_seal(orc, bytes(m), nonce, k)
+        ok = ok and lib.cz_box_open_afternm(back, c, mlen, nonce, k) == 0 and bytes(back) == bytes(m)
+        co, mb, nb = ctypes.create_string_buffer(mlen), bytes(m), bytes(nonce)
+        t_or = med(lambda: orc.or_secretbox(co, mb, mlen, nb, PRECOM), 400)
+        row = {"payload_bytes": n, "seal_us": round(t_seal * 1e6, 1), "open_us": round(t_open * 1e6, 1),
+               "oracle_1core_us": round(t_or * 1e6, 2), "verified": bool(ok)}
+        if sod is not None:
+            cs = (ctypes.c_uint8 * mlen)()
+            t_s = med(lambda: sod.crypto_box_afternm(cs, m, ctypes.c_ulonglong(mlen), nonce, k), 2000)
+            row["libsodium_1core_us"] = round(t_s * 1e6, 2)
+        rows.append(row)
+    # batched host-staged API at 4 KiB: per-call time for B messages
+    ctx = ctypes.c_void_p()
+    _lib.check(lib.cz_ctx_create(ctypes.byref(ctx), dev.index or 0), "cz_ctx_create")
+    _lib.check(lib.cz_ctx_set_keys(ctx, PRECOM, 1, _lib.CZ_DIR_C2S), "cz_ctx_set_keys")
+    bmax = 1 << 16
+    pin, pout = lib.cz_host_alloc(bmax * 4096), lib.cz_host_alloc(bmax * 4224)
+    batches = []
+    for B in (1, 4, 16, 64, 256, 1024, 4096, 16384, 65536):
+        t = med(lambda: _lib.check(lib.cz_ctx_seal_uniform(ctx, B, 4096, pin, 4096, pout, 4224, 3, None, 16384),
+                                   "seal"), 100)
+        batches.append({"batch": B, "call_us": round(t * 1e6, 1), "per_msg_us": round(t * 1e6 / B, 3),
+                        "GiBps": round(B * 4096 / t / 2**30, 3)})
+    lib.cz_ctx_destroy(ctx)
+    lib.cz_host_free(pin)
+    lib.cz_host_free(pout)
+    cpu_4k = next(r for r in rows if r["payload_bytes"] == 4096)
+    ref_us = cpu_4k.get("libsodium_1core_us", cpu_4k["oracle_1core_us"])
+    win = next((b["batch"] for b in batches if b["per_msg_us"] < ref_us), None)
+    return {"metric": "jnacl drop-in single-message latency (cz_box_afternm / open), host buffers",
+            "value": rows[1]["seal_us"], "unit": "us per 4 KiB message", "higher_is_better": False, "n_gpus": 1,
+            "ctypes_call_overhead_us": round(t_ctypes * 1e6, 2), "single_shot": rows, "batched_4k": batches,
+            "batch_beating_one_cpu_core": win,
+            "cpu_reference_for_crossover": "libsodium crypto_box_afternm, 1 core" if sod is not None else "oracle, 1 core"}
+
+
+def orc_seal(orc, m, nonce, k):
+    out = ctypes.create_string_buffer(len(m))
+    orc.or_secretbox(out, m, len(m), bytes(nonce), bytes(k))
+    return out.raw
 
 
 def beforenm_bench(args, dev):
@@ -539,8 +682,9 @@ def main():
     args = parse()
     world, rank, local = setup_dist(args)
     dev = torch.device(f"cuda:{local}")
-    if args.config in ("e2e4k", "engine", "beforenm"):
-        line = {"e2e4k": e2e_host, "engine": engine_host, "beforenm": beforenm_bench}[args.config](args, dev)
+    if args.config in ("e2e4k", "engine", "beforenm", "nacl"):
+        line = {"e2e4k": e2e_host, "engine": engine_host, "beforenm": beforenm_bench,
+                "nacl": nacl_latency}[args.config](args, dev)
         if rank == 0:
             print(json.dumps(line), flush=True)
         return

@@ -302,10 +302,20 @@ void *cz_engine_msg_alloc(cz_engine *e, uint32_t len);
 /* queue one Msg (payload from cz_engine_msg_alloc, or copied into the arena); CZ_ENOMEM when the
  * arena is full (flush first), CZ_EPROTO when the connection has failed */
 int cz_engine_send(cz_engine *e, int conn, const void *payload, uint32_t len, int msg_flags);
-/* seal every queued Msg on the device and pack each connection's MESSAGE frames, in send order,
- * into its wire stream (pinned host memory, valid until the next cz_engine_flush_out) */
+/* seal every queued Msg on the device and V2-frame it into one pinned output in SEND order
+ * (valid until the next cz_engine_flush_out).  The flush is pipelined in groups of ~8 MiB+:
+ * H2D of a group overlaps the seal + D2H of the one before. */
 int cz_engine_flush_out(cz_engine *e);
+/* one connection's MESSAGE frames, in its send order, as contiguous bytes: a pointer into the
+ * flush output when its messages were queued back to back, else a host-gathered copy */
 int cz_engine_wire_out(cz_engine *e, int conn, const uint8_t **wire, uint64_t *len);
+/* the same stream as gather-write pieces of the flush output (for writev / a GatheringByteChannel,
+ * StreamEngine.java:509-535): *count = pieces; fills iov when cap >= *count (cap 0: count only) */
+typedef struct cz_iovec {
+    const uint8_t *base;
+    uint64_t len;
+} cz_iovec;
+int cz_engine_wire_iov(cz_engine *e, int conn, cz_iovec *iov, uint32_t cap, uint32_t *count);
 /* append bytes received on a connection (partial frames are kept for the next flush) */
 int cz_engine_recv(cz_engine *e, int conn, const void *wire, uint64_t len);
 /* zero-copy receive (the V2Decoder getBuffer() pattern, StreamEngine.java:403-410): a pinned

@@ -132,6 +132,7 @@ SIGNATURES = {
     "cz_engine_send": (_I, [_VP, _I, _VP, _U32, _I]),
     "cz_engine_flush_out": (_I, [_VP]),
     "cz_engine_wire_out": (_I, [_VP, _I, ctypes.POINTER(_VP), ctypes.POINTER(_U64)]),
+    "cz_engine_wire_iov": (_I, [_VP, _I, _VP, _U32, ctypes.POINTER(_U32)]),
     "cz_engine_recv": (_I, [_VP, _I, _VP, _U64]),
     "cz_engine_recv_buffer": (_I, [_VP, _I, _U64, ctypes.POINTER(_VP), ctypes.POINTER(_U64)]),
     "cz_engine_recv_commit": (_I, [_VP, _I, _U64]),

@@ -84,6 +84,10 @@ struct PhaseTimer {
     }
 };
 
+struct Run {
+    uint64_t off, len;
+};
+
 struct Conn {
     bool server = false;
     uint32_t tx_key = 0, rx_key = 0;  // subkey table indices
@@ -93,7 +97,8 @@ struct Conn {
     int event = 0;                    // ZMTP protocol-error event of the failure
     HostBuf rx;                       // received bytes not yet parsed, pinned (DMA'd as they lie)
     uint64_t rx_len = 0;
-    uint64_t wire_off = 0, wire_len = 0;
+    std::vector<Run> runs;            // wire stream of the last flush_out: pieces of h_wire, in send order
+    std::vector<uint8_t> gathered;    // contiguous copy for cz_engine_wire_out when runs > 1
     std::vector<uint32_t> in_msgs;    // indices into Engine::in_msgs of the last flush_in
 };
 
@@ -118,22 +123,33 @@ struct Segs {
 
 int plan(const std::vector<cz_frame_desc> &d, int open, Segs &s)
 {
-    s.nseg = s.ncomb = s.npart = 0;
-    cz_plan_segments(d.data(), (uint32_t)d.size(), open, SEG_BLOCKS, nullptr, 0, &s.nseg, nullptr, 0, &s.ncomb,
-                     &s.npart);
+    plan_segments(d.data(), (uint32_t)d.size(), open, SEG_BLOCKS, s.seg, s.comb, s.npart);
+    s.nseg = (uint32_t)s.seg.size();
+    s.ncomb = (uint32_t)s.comb.size();
     s.seg.resize(std::max<uint32_t>(s.nseg, 1));
     s.comb.resize(std::max<uint32_t>(s.ncomb, 1));
-    return cz_plan_segments(d.data(), (uint32_t)d.size(), open, SEG_BLOCKS, s.seg.data(), (uint32_t)s.seg.size(),
-                            &s.nseg, s.comb.data(), (uint32_t)s.comb.size(), &s.ncomb, &s.npart);
+    return CZ_OK;
 }
+
+// destroys a flush's events on every return path
+struct EvGuard {
+    std::vector<hipEvent_t> &v;
+    ~EvGuard()
+    {
+        for (hipEvent_t x : v)
+            if (x)
+                (void)hipEventDestroy(x);
+    }
+};
 
 }  // namespace
 
 struct cz_engine {
     int device = 0;
     hipStream_t stream = nullptr;
-    // flush_in pipeline: ps[0] carries every group's H2D in order; ps[1] waits for a group's
-    // copies (event), then runs its kernels and D2H -- so group g's D2H overlaps group g+1's H2D
+    // flush pipelines: ps[0] carries every group's H2D in order; ps[1] waits for a group's copies
+    // (event) and runs its kernels; ps[2] waits for those (event) and carries the group's D2H -- so
+    // group g's D2H overlaps group g+1's H2D and kernels
     static constexpr int PIPE = 3;
     hipStream_t ps[PIPE] = {nullptr, nullptr, nullptr};
     std::vector<Conn> conns;
@@ -204,95 +220,164 @@ struct cz_engine {
         return hipSuccess;
     }
 
-    int upload_and_plan(const std::vector<cz_frame_desc> &desc, int open, Segs &s)
-    {
-        int rc = plan(desc, open, s);
-        if (rc != CZ_OK)
-            return rc;
-        hipError_t e;
-        if ((e = d_desc.reserve(desc.size() * sizeof(cz_frame_desc))) != hipSuccess ||
-            (e = d_seg.reserve((uint64_t)s.seg.size() * sizeof(cz_segment))) != hipSuccess ||
-            (e = d_comb.reserve((uint64_t)s.comb.size() * sizeof(cz_combine))) != hipSuccess ||
-            (e = d_work.reserve((uint64_t)std::max<uint32_t>(s.npart, 1) * 64)) != hipSuccess)
-            return hip_fail(e, "cz_engine: hipMalloc");
-        // the host vectors stay alive until the caller synchronises the stream
-        if ((e = hipMemcpyAsync(d_desc.ptr, desc.data(), desc.size() * sizeof(cz_frame_desc), hipMemcpyHostToDevice,
-                                stream)) != hipSuccess ||
-            (e = hipMemcpyAsync(d_seg.ptr, s.seg.data(), (uint64_t)s.nseg * sizeof(cz_segment), hipMemcpyHostToDevice,
-                                stream)) != hipSuccess ||
-            (s.ncomb && (e = hipMemcpyAsync(d_comb.ptr, s.comb.data(), (uint64_t)s.ncomb * sizeof(cz_combine),
-                                            hipMemcpyHostToDevice, stream)) != hipSuccess))
-            return hip_fail(e, "cz_engine: H2D");
-        return CZ_OK;
-    }
-
+    // Outbound pipeline.  The wire output is in SEND order: message i's V2 frame (header + body)
+    // sits at wpos[i], and each connection's stream is the list of its runs of consecutive frames
+    // (one run when the caller queued a connection's messages together, as StreamEngine.outEvent
+    // pulls one pipe at a time).  Send order lets the flush run in G groups of ~equal bytes:
+    // ps[0] copies group g's arena range and metadata while ps[1] seals + packs group g-1 and
+    // copies its wire bytes back, so H2D and D2H overlap instead of running back to back.
     int flush_out()
     {
         PhaseTimer pt("flush_out");
-        for (Conn &c : conns)
-            c.wire_off = c.wire_len = 0;
+        for (Conn &c : conns) {
+            c.runs.clear();
+            c.gathered.clear();
+        }
         wire_total = 0;
         const uint32_t n = (uint32_t)pend.size();
         if (n == 0) {
             arena_used = 0;  // buffers allocated but never sent are released too
             return CZ_OK;
         }
-        // wire layout: each connection's frames contiguous, in send order; connections in id order
-        std::vector<uint64_t> conn_bytes(conns.size(), 0);
-        for (const OutMsg &m : pend) {
-            const uint64_t body = (uint64_t)m.len + CZ_MESSAGE_OVERHEAD;
-            conn_bytes[m.conn] += cz_v2_header_size(body) + body;
-        }
-        uint64_t w = 0;
-        for (size_t c = 0; c < conns.size(); c++) {
-            conns[c].wire_off = w;
-            conns[c].wire_len = conn_bytes[c];
-            w += conn_bytes[c];
-        }
-        wire_total = w;
-        std::vector<uint64_t> cursor(conns.size());
-        for (size_t c = 0; c < conns.size(); c++)
-            cursor[c] = conns[c].wire_off;
         std::vector<cz_frame_desc> desc(n);
         std::vector<cz_v2_item> items(n);
-        uint64_t slot = 0;
+        std::vector<uint64_t> wpos(n + 1);
+        uint64_t w = 0;
         for (uint32_t i = 0; i < n; i++) {
             const OutMsg &m = pend[i];
             Conn &c = conns[m.conn];
             const uint64_t body = (uint64_t)m.len + CZ_MESSAGE_OVERHEAD;
-            desc[i] = {m.arena_off, slot, m.len, c.tx_key, c.nonce++, m.flags & 0xffu, -1};
-            items[i] = {slot, cursor[m.conn], (uint32_t)body, (uint32_t)CZ_V2_ITEM_HEADER};
-            cursor[m.conn] += cz_v2_header_size(body) + body;
-            slot += round_up(body, SLOT_ALIGN);
+            const uint64_t fb = cz_v2_header_size(body) + body;
+            wpos[i] = w;
+            if (!c.runs.empty() && c.runs.back().off + c.runs.back().len == w)
+                c.runs.back().len += fb;
+            else
+                c.runs.push_back({w, fb});
+            w += fb;
         }
-        pt.mark("desc");
+        wpos[n] = w;
+        wire_total = w;
+        // groups of ~equal wire bytes: [fa, fb) in send order, body slots contiguous per group
+        struct Group {
+            uint32_t fa, fb;
+            uint64_t arena_hi;  // the arena prefix [0, arena_hi) holds every payload of groups <= this one
+        };
+        std::vector<Group> groups;
+        {
+            const uint64_t G = std::min<uint64_t>(8, std::max<uint64_t>(1, w / (8ull << 20)));
+            uint32_t fa = 0;
+            for (uint32_t i = 0; i < n; i++)
+                if (i + 1 == n || wpos[i + 1] * G >= w * (groups.size() + 1)) {
+                    groups.push_back({fa, i + 1, 0});
+                    fa = i + 1;
+                }
+        }
+        uint64_t slot = 0, hi = 0;
+        for (Group &g : groups) {
+            for (uint32_t i = g.fa; i < g.fb; i++) {
+                const OutMsg &m = pend[i];
+                Conn &c = conns[m.conn];
+                const uint64_t body = (uint64_t)m.len + CZ_MESSAGE_OVERHEAD;
+                desc[i] = {m.arena_off, slot, m.len, c.tx_key, c.nonce++, m.flags & 0xffu, -1};
+                items[i] = {slot, wpos[i], (uint32_t)body, (uint32_t)CZ_V2_ITEM_HEADER};
+                slot += round_up(body, SLOT_ALIGN);
+                hi = std::max<uint64_t>(hi, m.arena_off + m.len);
+            }
+            g.arena_hi = hi;
+        }
+        // segment / combine counts per group (the plans themselves are made inside the loop, each
+        // while the copies issued before it run); the device arrays hold all groups at once
+        std::vector<uint64_t> soff(groups.size() + 1, 0), coff(groups.size() + 1, 0), woff(groups.size() + 1, 0);
+        for (size_t gi = 0; gi < groups.size(); gi++) {
+            uint64_t ns = 0, nc = 0, np = 0;
+            for (uint32_t i = groups[gi].fa; i < groups[gi].fb; i++)
+                plan_counts(desc[i].len, 0, SEG_BLOCKS, ns, nc, np);
+            soff[gi + 1] = soff[gi] + ns;
+            coff[gi + 1] = coff[gi] + nc;
+            woff[gi + 1] = woff[gi] + np;
+        }
+        const uint64_t nseg = soff[groups.size()], ncomb = coff[groups.size()], npart = woff[groups.size()];
+        const uint64_t m_items = 0, m_desc = (uint64_t)n * sizeof(cz_v2_item),
+                       m_seg = m_desc + (uint64_t)n * sizeof(cz_frame_desc), m_comb = m_seg + nseg * sizeof(cz_segment),
+                       m_end = m_comb + ncomb * sizeof(cz_combine);
         hipError_t e;
         if ((e = d_in.reserve(std::max<uint64_t>(arena_used, 16))) != hipSuccess ||
             (e = d_body.reserve(slot)) != hipSuccess || (e = d_wire.reserve(wire_total)) != hipSuccess ||
             (e = d_items.reserve((uint64_t)n * sizeof(cz_v2_item))) != hipSuccess ||
-            (e = h_wire.reserve(wire_total)) != hipSuccess)
+            (e = d_desc.reserve((uint64_t)n * sizeof(cz_frame_desc))) != hipSuccess ||
+            (e = d_seg.reserve(std::max<uint64_t>(nseg, 1) * sizeof(cz_segment))) != hipSuccess ||
+            (e = d_comb.reserve(std::max<uint64_t>(ncomb, 1) * sizeof(cz_combine))) != hipSuccess ||
+            (e = d_work.reserve(std::max<uint64_t>(npart, 1) * 64)) != hipSuccess ||
+            (e = h_wire.reserve(wire_total)) != hipSuccess || (e = h_meta.reserve(m_end)) != hipSuccess)
             return hip_fail(e, "cz_engine: alloc");
-        if ((e = hipMemcpyAsync(d_in.ptr, arena.ptr, arena_used, hipMemcpyHostToDevice, stream)) != hipSuccess ||
-            (e = hipMemcpyAsync(d_items.ptr, items.data(), (uint64_t)n * sizeof(cz_v2_item), hipMemcpyHostToDevice,
-                                stream)) != hipSuccess)
+        // pinned copies of the host-built arrays: pageable sources would make each H2D synchronous
+        uint8_t *hm = (uint8_t *)h_meta.ptr;
+        memcpy(hm + m_items, items.data(), (uint64_t)n * sizeof(cz_v2_item));
+        memcpy(hm + m_desc, desc.data(), (uint64_t)n * sizeof(cz_frame_desc));
+        pt.mark("desc");
+        std::vector<hipEvent_t> ev(groups.size(), nullptr), evk(groups.size(), nullptr);
+        EvGuard evguard{ev}, evkguard{evk};
+        for (size_t gi = 0; gi < groups.size(); gi++)
+            if ((e = hipEventCreateWithFlags(&ev[gi], hipEventDisableTiming)) != hipSuccess ||
+                (e = hipEventCreateWithFlags(&evk[gi], hipEventDisableTiming)) != hipSuccess)
+                return hip_fail(e, "hipEventCreate");
+        hipStream_t qh = ps[0], qk = ps[1], qo = ps[2];
+        uint64_t copied = 0;
+        // the arena bytes not copied yet up to group g's last payload
+        auto copy_arena = [&](size_t gi) -> hipError_t {
+            if (gi >= groups.size() || groups[gi].arena_hi <= copied)
+                return hipSuccess;
+            hipError_t r = hipMemcpyAsync((uint8_t *)d_in.ptr + copied, (const uint8_t *)arena.ptr + copied,
+                                          groups[gi].arena_hi - copied, hipMemcpyHostToDevice, qh);
+            copied = groups[gi].arena_hi;
+            return r;
+        };
+        if ((e = copy_arena(0)) != hipSuccess)
             return hip_fail(e, "cz_engine: H2D");
-        Segs s;
-        int rc = upload_and_plan(desc, 0, s);
-        if (rc != CZ_OK)
-            return rc;
-        pt.mark("h2d+plan");
-        if ((e = czk_seal_segments((const cz_frame_desc *)d_desc.ptr, (const cz_segment *)d_seg.ptr, s.nseg,
-                                   (const cz_combine *)d_comb.ptr, s.ncomb, d_in.ptr, d_body.ptr, subkeys.ptr,
-                                   d_work.ptr, stream)) != hipSuccess ||
-            (e = czk_v2_copy((const cz_v2_item *)d_items.ptr, n, d_body.ptr, d_wire.ptr, stream)) != hipSuccess)
-            return hip_fail(e, "cz_engine: flush_out");
-        if (pt.on && (e = hipStreamSynchronize(stream)) != hipSuccess)
-            return hip_fail(e, "cz_engine: flush_out");
-        pt.mark("kernels");
-        if ((e = hipMemcpyAsync(h_wire.ptr, d_wire.ptr, wire_total, hipMemcpyDeviceToHost, stream)) != hipSuccess ||
-            (e = hipStreamSynchronize(stream)) != hipSuccess)
-            return hip_fail(e, "cz_engine: flush_out");
-        pt.mark("d2h");
+        Segs sg;
+        for (size_t gi = 0; gi < groups.size(); gi++) {
+            const Group &g = groups[gi];
+            const uint32_t gn = g.fb - g.fa;
+            plan_segments(desc.data() + g.fa, gn, 0, SEG_BLOCKS, sg.seg, sg.comb, sg.npart);
+            const uint32_t gseg = (uint32_t)sg.seg.size(), gcomb = (uint32_t)sg.comb.size();
+            memcpy(hm + m_seg + soff[gi] * sizeof(cz_segment), sg.seg.data(), (uint64_t)gseg * sizeof(cz_segment));
+            memcpy(hm + m_comb + coff[gi] * sizeof(cz_combine), sg.comb.data(), (uint64_t)gcomb * sizeof(cz_combine));
+            if (gseg != soff[gi + 1] - soff[gi] || gcomb != coff[gi + 1] - coff[gi] || sg.npart != woff[gi + 1] - woff[gi])
+                return fail(CZ_EINVAL, "cz_engine: segment plan disagrees with its count");
+            cz_frame_desc *dd = (cz_frame_desc *)d_desc.ptr + g.fa;
+            cz_segment *dsg = (cz_segment *)d_seg.ptr + soff[gi];
+            cz_combine *dcb = (cz_combine *)d_comb.ptr + coff[gi];
+            // (a) copy stream: the group's metadata, then the next group's arena bytes (copied while
+            //     the host plans that group)
+            if ((e = hipMemcpyAsync((cz_v2_item *)d_items.ptr + g.fa, (const cz_v2_item *)(hm + m_items) + g.fa,
+                                    (uint64_t)gn * sizeof(cz_v2_item), hipMemcpyHostToDevice, qh)) != hipSuccess ||
+                (e = hipMemcpyAsync(dd, (const cz_frame_desc *)(hm + m_desc) + g.fa, (uint64_t)gn * sizeof(cz_frame_desc),
+                                    hipMemcpyHostToDevice, qh)) != hipSuccess ||
+                (gseg && (e = hipMemcpyAsync(dsg, (const cz_segment *)(hm + m_seg) + soff[gi],
+                                             (uint64_t)gseg * sizeof(cz_segment), hipMemcpyHostToDevice, qh)) !=
+                             hipSuccess) ||
+                (gcomb && (e = hipMemcpyAsync(dcb, (const cz_combine *)(hm + m_comb) + coff[gi],
+                                              (uint64_t)gcomb * sizeof(cz_combine), hipMemcpyHostToDevice, qh)) !=
+                              hipSuccess) ||
+                (e = hipEventRecord(ev[gi], qh)) != hipSuccess || (e = copy_arena(gi + 1)) != hipSuccess)
+                return hip_fail(e, "cz_engine: flush_out H2D");
+            // (b) compute stream: seal into body slots, pack behind V2 headers at the send-order
+            //     wire positions; (c) D2H stream: the group's wire bytes back
+            if ((e = hipStreamWaitEvent(qk, ev[gi], 0)) != hipSuccess ||
+                (e = czk_seal_segments(dd, dsg, gseg, dcb, gcomb, d_in.ptr, d_body.ptr, subkeys.ptr,
+                                       (uint8_t *)d_work.ptr + 64 * woff[gi], qk)) != hipSuccess ||
+                (e = czk_v2_copy((const cz_v2_item *)d_items.ptr + g.fa, gn, d_body.ptr, d_wire.ptr, qk)) !=
+                    hipSuccess ||
+                (e = hipEventRecord(evk[gi], qk)) != hipSuccess ||
+                (e = hipStreamWaitEvent(qo, evk[gi], 0)) != hipSuccess ||
+                (e = hipMemcpyAsync((uint8_t *)h_wire.ptr + wpos[g.fa], (uint8_t *)d_wire.ptr + wpos[g.fa],
+                                    wpos[g.fb] - wpos[g.fa], hipMemcpyDeviceToHost, qo)) != hipSuccess)
+                return hip_fail(e, "cz_engine: flush_out");
+        }
+        for (hipStream_t q : ps)
+            if ((e = hipStreamSynchronize(q)) != hipSuccess)
+                return hip_fail(e, "cz_engine: flush_out");
+        pt.mark("h2d+kernels+d2h");
         pend.clear();
         arena_used = 0;
         return CZ_OK;
@@ -314,21 +399,70 @@ struct cz_engine {
         in_msgs.clear();
         for (Conn &c : conns)
             c.in_msgs.clear();
-        // 1. parse every connection's whole frames (V2Decoder), gather them into one staging buffer
+        // 0. the live connections' received bytes, in groups of ~equal bytes.  Each group's H2D
+        //    (whole receive buffers, DMA'd straight from the pinned per-connection buffers) is
+        //    issued before any parsing, so the copies run while the host parses and plans.
         struct Parsed {
             uint32_t conn;
             uint32_t first, count;  // range in frames
-            uint64_t rx_off;        // where the connection's whole-frame bytes start in d_wire
-            uint64_t consumed;
+            uint64_t rx_off;        // where the connection's received bytes start in d_wire
+            uint64_t consumed;      // whole frames
             int perr;               // framing error after the parsed frames
         };
         std::vector<Parsed> parsed;
-        std::vector<cz_v2_frame> frames;
         uint64_t rx_total = 0;
         for (size_t ci = 0; ci < conns.size(); ci++) {
             Conn &c = conns[ci];
             if (c.error || c.rx_len == 0)
                 continue;
+            parsed.push_back({(uint32_t)ci, 0u, 0u, rx_total, 0u, 0});
+            rx_total += c.rx_len;
+        }
+        struct Group {
+            size_t pa, pb;        // parsed[pa, pb)
+            uint32_t fa, fb;      // frames[fa, fb)
+            uint64_t pl0, pl1;    // plaintext slot range
+        };
+        std::vector<Group> groups;
+        {
+            const int G = rx_total >= (64ull << 20) ? 8 : 1;
+            size_t pa = 0;
+            uint64_t acc = 0;
+            for (size_t q = 0; q < parsed.size(); q++) {
+                acc += conns[parsed[q].conn].rx_len;
+                if (q + 1 == parsed.size() || acc * G >= rx_total * (groups.size() + 1)) {
+                    groups.push_back({pa, q + 1, 0, 0, 0, 0});
+                    pa = q + 1;
+                }
+            }
+        }
+        hipError_t e;
+        std::vector<hipEvent_t> ev(groups.size(), nullptr), evm(groups.size(), nullptr), evk(groups.size(), nullptr);
+        EvGuard evguard{ev}, evmguard{evm}, evkguard{evk};
+        for (size_t gi = 0; gi < groups.size(); gi++)
+            if ((e = hipEventCreateWithFlags(&ev[gi], hipEventDisableTiming)) != hipSuccess ||
+                (e = hipEventCreateWithFlags(&evm[gi], hipEventDisableTiming)) != hipSuccess ||
+                (e = hipEventCreateWithFlags(&evk[gi], hipEventDisableTiming)) != hipSuccess)
+                return hip_fail(e, "hipEventCreate");
+        // ps[0]: received bytes H2D; stream: metadata H2D; ps[1]: kernels; ps[2]: D2H
+        hipStream_t qh = ps[0], qk = ps[1], qo = ps[2], qm = stream;
+        if (rx_total && (e = d_wire.reserve(rx_total)) != hipSuccess)
+            return hip_fail(e, "cz_engine: alloc");
+        for (size_t gi = 0; gi < groups.size(); gi++) {
+            for (size_t pi = groups[gi].pa; pi < groups[gi].pb; pi++) {
+                const Parsed &p = parsed[pi];
+                if ((e = hipMemcpyAsync((uint8_t *)d_wire.ptr + p.rx_off, conns[p.conn].rx.ptr, conns[p.conn].rx_len,
+                                        hipMemcpyHostToDevice, qh)) != hipSuccess)
+                    return hip_fail(e, "cz_engine: H2D");
+            }
+            if ((e = hipEventRecord(ev[gi], qh)) != hipSuccess)
+                return hip_fail(e, "cz_engine: H2D");
+        }
+        pt.mark("h2d-issue");
+        // 1. parse every connection's whole frames (V2Decoder); a partial frame waits for more bytes
+        std::vector<cz_v2_frame> frames;
+        for (Parsed &p : parsed) {
+            const Conn &c = conns[p.conn];
             // parse in chunks of CH frames (a frame is >= 2 bytes, so sizing by bytes would cost 8x the data)
             constexpr uint32_t CH = 4096;
             const size_t base = frames.size();
@@ -348,39 +482,20 @@ struct cz_engine {
                 if (prc != CZ_OK || nf < CH)
                     break;
             }
-            const uint32_t nf = (uint32_t)(frames.size() - base);
-            parsed.push_back({(uint32_t)ci, (uint32_t)base, nf, rx_total, consumed, prc == CZ_OK ? 0 : prc});
-            rx_total += consumed;
+            p.first = (uint32_t)base;
+            p.count = (uint32_t)(frames.size() - base);
+            p.consumed = consumed;
+            p.perr = prc == CZ_OK ? 0 : prc;
         }
         const uint32_t n = (uint32_t)frames.size();
-        hipError_t e;
         pt.mark("parse");
-        // 2. connection groups of ~equal bytes (pipelined below), then descriptors: bodies unpacked
-        //    into aligned slots, each connection's frames chained by prev (group-relative indices)
-        struct Group {
-            size_t pa, pb;        // parsed[pa, pb)
-            uint32_t fa, fb;      // frames[fa, fb)
-            uint64_t pl0, pl1;    // plaintext slot range
-        };
-        std::vector<Group> groups;
-        {
-            const int G = rx_total >= (64ull << 20) ? 8 : 1;
-            size_t pa = 0;
-            uint64_t acc = 0;
-            for (size_t q = 0; q < parsed.size(); q++) {
-                acc += parsed[q].consumed;
-                const bool last = q + 1 == parsed.size();
-                if (last || acc * G >= rx_total * (groups.size() + 1)) {
-                    groups.push_back({pa, q + 1, 0, 0, 0, 0});
-                    pa = q + 1;
-                }
-            }
-        }
+        // 2. descriptors: bodies unpacked into aligned slots, each connection's frames chained by
+        //    prev (group-relative indices)
         std::vector<cz_frame_desc> desc(n);
         std::vector<cz_v2_item> items(n);
         uint64_t bslot = 0, pslot = 0;
         for (Group &g : groups) {
-            g.fa = g.pa < parsed.size() ? parsed[g.pa].first : n;
+            g.fa = parsed[g.pa].first;
             g.pl0 = pslot;
             for (size_t q = g.pa; q < g.pb; q++) {
                 const Parsed &p = parsed[q];
@@ -396,28 +511,19 @@ struct cz_engine {
                     pslot += round_up(std::max<uint64_t>(plen, 1), SLOT_ALIGN);
                 }
             }
-            g.fb = g.pb > g.pa ? parsed[g.pb - 1].first + parsed[g.pb - 1].count : g.fa;
+            g.fb = parsed[g.pb - 1].first + parsed[g.pb - 1].count;
             g.pl1 = pslot;
         }
         if (n) {
-            if ((e = d_wire.reserve(rx_total)) != hipSuccess || (e = d_in.reserve(bslot)) != hipSuccess ||
-                (e = d_plain.reserve(pslot)) != hipSuccess ||
-                (e = d_items.reserve((uint64_t)n * sizeof(cz_v2_item))) != hipSuccess ||
-                (e = d_status.reserve((uint64_t)n * 2)) != hipSuccess ||
-                (e = d_nonces.reserve((uint64_t)n * 8)) != hipSuccess ||
-                (e = h_plain.reserve(pslot)) != hipSuccess || (e = h_status.reserve((uint64_t)n * 2)) != hipSuccess ||
-                (e = h_nonces.reserve((uint64_t)n * 8)) != hipSuccess)
-                return hip_fail(e, "cz_engine: alloc");
             // plans per group; device segment / combine / work arrays hold all groups at once
             std::vector<Segs> gs(groups.size());
             uint64_t nseg = 0, ncomb = 0, npart = 0;
             std::vector<uint64_t> soff(groups.size()), coff(groups.size()), woff(groups.size());
             for (size_t gi = 0; gi < groups.size(); gi++) {
                 const Group &g = groups[gi];
-                std::vector<cz_frame_desc> sub(desc.begin() + g.fa, desc.begin() + g.fb);
-                int rc = plan(sub, 1, gs[gi]);
-                if (rc != CZ_OK)
-                    return rc;
+                plan_segments(desc.data() + g.fa, g.fb - g.fa, 1, SEG_BLOCKS, gs[gi].seg, gs[gi].comb, gs[gi].npart);
+                gs[gi].nseg = (uint32_t)gs[gi].seg.size();
+                gs[gi].ncomb = (uint32_t)gs[gi].comb.size();
                 soff[gi] = nseg;
                 coff[gi] = ncomb;
                 woff[gi] = npart;
@@ -425,16 +531,23 @@ struct cz_engine {
                 ncomb += gs[gi].ncomb;
                 npart += gs[gi].npart;
             }
-            // pinned copies of the host-built arrays: pageable sources would make each H2D synchronous
             const uint64_t m_items = 0, m_desc = (uint64_t)n * sizeof(cz_v2_item),
                            m_seg = m_desc + (uint64_t)n * sizeof(cz_frame_desc),
                            m_comb = m_seg + nseg * sizeof(cz_segment), m_end = m_comb + ncomb * sizeof(cz_combine);
-            if ((e = d_desc.reserve((uint64_t)n * sizeof(cz_frame_desc))) != hipSuccess ||
+            // (a device buffer that has to grow is reallocated here, which waits for the copies
+            //  in flight; steady-state flushes reuse their buffers)
+            if ((e = d_in.reserve(bslot)) != hipSuccess || (e = d_plain.reserve(pslot)) != hipSuccess ||
+                (e = d_items.reserve((uint64_t)n * sizeof(cz_v2_item))) != hipSuccess ||
+                (e = d_status.reserve((uint64_t)n * 2)) != hipSuccess ||
+                (e = d_nonces.reserve((uint64_t)n * 8)) != hipSuccess ||
+                (e = d_desc.reserve((uint64_t)n * sizeof(cz_frame_desc))) != hipSuccess ||
                 (e = d_seg.reserve(std::max<uint64_t>(nseg, 1) * sizeof(cz_segment))) != hipSuccess ||
                 (e = d_comb.reserve(std::max<uint64_t>(ncomb, 1) * sizeof(cz_combine))) != hipSuccess ||
                 (e = d_work.reserve(std::max<uint64_t>(npart, 1) * 64)) != hipSuccess ||
-                (e = h_meta.reserve(m_end)) != hipSuccess)
+                (e = h_plain.reserve(pslot)) != hipSuccess || (e = h_status.reserve((uint64_t)n * 2)) != hipSuccess ||
+                (e = h_nonces.reserve((uint64_t)n * 8)) != hipSuccess || (e = h_meta.reserve(m_end)) != hipSuccess)
                 return hip_fail(e, "cz_engine: alloc");
+            // pinned copies of the host-built arrays: pageable sources would make each H2D synchronous
             uint8_t *hm = (uint8_t *)h_meta.ptr;
             memcpy(hm + m_items, items.data(), (uint64_t)n * sizeof(cz_v2_item));
             memcpy(hm + m_desc, desc.data(), (uint64_t)n * sizeof(cz_frame_desc));
@@ -449,66 +562,49 @@ struct cz_engine {
             const cz_segment *h_seg = (const cz_segment *)(hm + m_seg);
             const cz_combine *h_comb = (const cz_combine *)(hm + m_comb);
             pt.mark("desc+plan");
-            std::vector<hipEvent_t> ev(groups.size(), nullptr);
-            for (hipEvent_t &x : ev)
-                if ((e = hipEventCreateWithFlags(&x, hipEventDisableTiming)) != hipSuccess)
-                    return hip_fail(e, "hipEventCreate");
-            struct EvGuard {
-                std::vector<hipEvent_t> &v;
-                ~EvGuard()
-                {
-                    for (hipEvent_t x : v)
-                        if (x)
-                            (void)hipEventDestroy(x);
-                }
-            } evguard{ev};
-            hipStream_t qh = ps[0], qk = ps[1];
             for (size_t gi = 0; gi < groups.size(); gi++) {
                 const Group &g = groups[gi];
                 const uint32_t gn = g.fb - g.fa;
-                // (a) copy stream: the group's received bytes (straight from each connection's pinned
-                //     buffer) and its descriptors / items / segment lists
-                for (size_t pi = g.pa; pi < g.pb; pi++) {
-                    const Parsed &p = parsed[pi];
-                    if (p.consumed && (e = hipMemcpyAsync((uint8_t *)d_wire.ptr + p.rx_off, conns[p.conn].rx.ptr,
-                                                          p.consumed, hipMemcpyHostToDevice, qh)) != hipSuccess)
-                        return hip_fail(e, "cz_engine: H2D");
-                }
                 if (gn == 0)
                     continue;
                 const Segs &sg = gs[gi];
                 cz_frame_desc *dd = (cz_frame_desc *)d_desc.ptr + g.fa;
                 cz_segment *dsg = (cz_segment *)d_seg.ptr + soff[gi];
                 cz_combine *dcb = (cz_combine *)d_comb.ptr + coff[gi];
+                // (a) metadata stream: the group's descriptors / items / segment lists
                 if ((e = hipMemcpyAsync((cz_v2_item *)d_items.ptr + g.fa, h_items + g.fa,
-                                        (uint64_t)gn * sizeof(cz_v2_item), hipMemcpyHostToDevice, qh)) != hipSuccess ||
+                                        (uint64_t)gn * sizeof(cz_v2_item), hipMemcpyHostToDevice, qm)) != hipSuccess ||
                     (e = hipMemcpyAsync(dd, h_desc + g.fa, (uint64_t)gn * sizeof(cz_frame_desc),
-                                        hipMemcpyHostToDevice, qh)) != hipSuccess ||
+                                        hipMemcpyHostToDevice, qm)) != hipSuccess ||
                     (sg.nseg && (e = hipMemcpyAsync(dsg, h_seg + soff[gi], (uint64_t)sg.nseg * sizeof(cz_segment),
-                                                    hipMemcpyHostToDevice, qh)) != hipSuccess) ||
+                                                    hipMemcpyHostToDevice, qm)) != hipSuccess) ||
                     (sg.ncomb && (e = hipMemcpyAsync(dcb, h_comb + coff[gi], (uint64_t)sg.ncomb * sizeof(cz_combine),
-                                                     hipMemcpyHostToDevice, qh)) != hipSuccess) ||
-                    (e = hipEventRecord(ev[gi], qh)) != hipSuccess)
+                                                     hipMemcpyHostToDevice, qm)) != hipSuccess) ||
+                    (e = hipEventRecord(evm[gi], qm)) != hipSuccess)
                     return hip_fail(e, "cz_engine: flush_in H2D");
-                // (b) compute stream: once the group's copies landed, unpack + open, then D2H
+                // (b) compute stream: once the group's bytes and metadata landed, unpack + open;
+                // (c) D2H stream
                 if ((e = hipStreamWaitEvent(qk, ev[gi], 0)) != hipSuccess ||
+                    (e = hipStreamWaitEvent(qk, evm[gi], 0)) != hipSuccess ||
                     (e = czk_v2_copy((const cz_v2_item *)d_items.ptr + g.fa, gn, d_wire.ptr, d_in.ptr, qk)) !=
                         hipSuccess ||
                     (e = czk_open_segments(dd, dsg, sg.nseg, dcb, sg.ncomb, d_in.ptr, d_plain.ptr, subkeys.ptr,
                                            (uint8_t *)d_work.ptr + 64 * woff[gi], (uint16_t *)d_status.ptr + g.fa,
                                            (uint64_t *)d_nonces.ptr + g.fa, qk)) != hipSuccess ||
+                    (e = hipEventRecord(evk[gi], qk)) != hipSuccess ||
+                    (e = hipStreamWaitEvent(qo, evk[gi], 0)) != hipSuccess ||
                     (e = hipMemcpyAsync((uint8_t *)h_plain.ptr + g.pl0, (uint8_t *)d_plain.ptr + g.pl0,
-                                        g.pl1 - g.pl0, hipMemcpyDeviceToHost, qk)) != hipSuccess ||
+                                        g.pl1 - g.pl0, hipMemcpyDeviceToHost, qo)) != hipSuccess ||
                     (e = hipMemcpyAsync((uint16_t *)h_status.ptr + g.fa, (uint16_t *)d_status.ptr + g.fa,
-                                        (uint64_t)gn * 2, hipMemcpyDeviceToHost, qk)) != hipSuccess ||
+                                        (uint64_t)gn * 2, hipMemcpyDeviceToHost, qo)) != hipSuccess ||
                     (e = hipMemcpyAsync((uint64_t *)h_nonces.ptr + g.fa, (uint64_t *)d_nonces.ptr + g.fa,
-                                        (uint64_t)gn * 8, hipMemcpyDeviceToHost, qk)) != hipSuccess)
+                                        (uint64_t)gn * 8, hipMemcpyDeviceToHost, qo)) != hipSuccess)
                     return hip_fail(e, "cz_engine: flush_in");
             }
-            for (hipStream_t q : ps)
-                if ((e = hipStreamSynchronize(q)) != hipSuccess)
-                    return hip_fail(e, "cz_engine: flush_in");
         }
+        for (hipStream_t q : {qh, qk, qo, qm})
+            if ((e = hipStreamSynchronize(q)) != hipSuccess)
+                return hip_fail(e, "cz_engine: flush_in");
         pt.mark("h2d+kernels+d2h");
         // 3. deliver in order per connection, up to the first failure (decodeAndPush returns false)
         const uint16_t *st = (const uint16_t *)h_status.ptr;
@@ -681,8 +777,41 @@ int cz_engine_wire_out(cz_engine *e, int conn, const uint8_t **wire, uint64_t *l
     Conn *c = e->conn(conn);
     if (!c)
         return CZ_EINVAL;
-    *wire = (const uint8_t *)e->h_wire.ptr + c->wire_off;
-    *len = c->wire_len;
+    const uint8_t *base = (const uint8_t *)e->h_wire.ptr;
+    if (c->runs.size() <= 1) {  // frames queued together: the stream lies in the flush output as is
+        *wire = c->runs.empty() ? base : base + c->runs[0].off;
+        *len = c->runs.empty() ? 0 : c->runs[0].len;
+        return CZ_OK;
+    }
+    if (c->gathered.empty()) {  // interleaved with other connections: one host gather
+        uint64_t t = 0;
+        for (const Run &r : c->runs)
+            t += r.len;
+        c->gathered.resize(t);
+        t = 0;
+        for (const Run &r : c->runs) {
+            memcpy(c->gathered.data() + t, base + r.off, r.len);
+            t += r.len;
+        }
+    }
+    *wire = c->gathered.data();
+    *len = c->gathered.size();
+    return CZ_OK;
+}
+
+int cz_engine_wire_iov(cz_engine *e, int conn, cz_iovec *iov, uint32_t cap, uint32_t *count)
+{
+    if (!e || !count || (cap && !iov))
+        return fail(CZ_EINVAL, "cz_engine_wire_iov: null pointer");
+    Conn *c = e->conn(conn);
+    if (!c)
+        return CZ_EINVAL;
+    *count = (uint32_t)c->runs.size();
+    if (cap < c->runs.size())
+        return cap ? fail(CZ_EINVAL, "cz_engine_wire_iov: %u pieces, capacity %u", *count, cap) : CZ_OK;
+    const uint8_t *base = (const uint8_t *)e->h_wire.ptr;
+    for (size_t k = 0; k < c->runs.size(); k++)
+        iov[k] = {base + c->runs[k].off, c->runs[k].len};
     return CZ_OK;
 }
 

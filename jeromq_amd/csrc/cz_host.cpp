@@ -273,6 +273,73 @@ static int nacl_one(uint8_t *dst, const uint8_t *src, uint64_t len, const uint8_
 
 }  // namespace czi
 
+namespace czi {
+
+// The segment planner (cz_plan_segments) in one pass, into vectors: the engine plans each
+// pipeline group while the copies of the previous one run.
+void plan_segments(const cz_frame_desc *h_desc, uint32_t count, int open, uint32_t seg_blocks,
+                   std::vector<cz_segment> &segs, std::vector<cz_combine> &combs, uint32_t &npart)
+{
+    segs.clear();
+    combs.clear();
+    const uint32_t split_above = seg_blocks + seg_blocks / 2;
+    segs.reserve(count);
+    uint32_t parts = 0;
+    for (uint32_t i = 0; i < count; i++) {
+        const uint64_t mlen = open ? (uint64_t)h_desc[i].len : (uint64_t)h_desc[i].len + CZ_MESSAGE_OVERHEAD;
+        uint32_t nblk = (uint32_t)((mlen + 63) / 64);
+        if (nblk == 0)
+            nblk = 1;
+        if (nblk <= split_above) {
+            segs.push_back({i, 0u, nblk, 0xffffffffu});
+            continue;
+        }
+        // Seal segment s covers box blocks [s*seg, (s+1)*seg).  Open segments s >= 1 start one
+        // block later, at s*seg + 1, so each one's payload chunks start at s*seg: the 33-byte
+        // shift puts payload chunk g across box blocks g and g+1.  Last segment: the remainder.
+        const uint32_t lead = open ? 1u : 0u;
+        const uint32_t ns = (nblk - lead + seg_blocks - 1) / seg_blocks;
+        combs.push_back({i, parts, ns, 0u});
+        for (uint32_t s = 0; s < ns; s++) {
+            const uint32_t b0 = s ? s * seg_blocks + lead : 0u;
+            const uint32_t b1 = s + 1 < ns ? (s + 1) * seg_blocks + lead : nblk;
+            segs.push_back({i, b0, b1 - b0, parts + s});
+        }
+        parts += ns;
+    }
+    // longest first, keyed on the kernel's loop count (output chunks), so that waves hold
+    // equal-length segments and can take the line-staged store path
+    auto chunks = [&](const cz_segment &g) -> uint32_t {
+        if (!open)
+            return g.nblocks;
+        const uint32_t len = h_desc[g.frame].len;
+        if (len < CZ_MESSAGE_OVERHEAD)
+            return 0u;
+        const uint32_t nblk = (len + 63) / 64, bend = g.first_block + g.nblocks;
+        const uint32_t cb = g.first_block ? g.first_block - 1 : 0u;
+        const uint32_t ce = bend == nblk ? (len - CZ_MESSAGE_OVERHEAD + 63) / 64 : bend - 1;
+        return ce - cb;
+    };
+    // Seal, within one length: segments whose input starts on a 128-byte line first, then the
+    // ones starting 64 bytes into a line, so that waves hold one line phase and the odd ones
+    // can read whole lines (seal_segment in cz_kernels.hip).  Key: chunks * 2 + (1 - phase).
+    auto phase = [&](const cz_segment &g) -> uint32_t {
+        return open ? 0u : (uint32_t)(((h_desc[g.frame].in_off + 64ull * g.first_block) >> 6) & 1u);
+    };
+    std::vector<std::pair<uint64_t, uint32_t>> key(segs.size());
+    for (size_t k = 0; k < segs.size(); k++)
+        key[k] = {2ull * chunks(segs[k]) + (1u - phase(segs[k])), (uint32_t)k};
+    std::stable_sort(key.begin(), key.end(), [](const std::pair<uint64_t, uint32_t> &a,
+                                                 const std::pair<uint64_t, uint32_t> &b) { return a.first > b.first; });
+    std::vector<cz_segment> sorted(segs.size());
+    for (size_t k = 0; k < segs.size(); k++)
+        sorted[k] = segs[key[k].second];
+    segs.swap(sorted);
+    npart = parts;
+}
+
+}  // namespace czi
+
 using namespace czi;
 
 // ---- cz_ctx ----------------------------------------------------------------
@@ -282,10 +349,12 @@ struct cz_ctx {
     DevBuf desc, in, out, status, keys, subkeys;
     HostBuf hdesc;
     uint32_t nkeys = 0;
-    // pipelined uniform batches: PIPE streams, each with its own chunk buffers
-    static constexpr int PIPE = 3;
+    // pipelined uniform batches: one stream per role (H2D, kernels, D2H) and NB chunk buffer sets
+    // used round robin; events order the reuse of each set across the three streams
+    static constexpr int PIPE = 3, NB = 4;
     hipStream_t ps[PIPE] = {nullptr, nullptr, nullptr};
-    DevBuf pin[PIPE], pout[PIPE], pflags[PIPE], pstatus[PIPE];
+    hipEvent_t ev_in[NB] = {}, ev_kern[NB] = {}, ev_out[NB] = {};
+    DevBuf pin[NB], pout[NB], pflags[NB], pstatus[NB];
 };
 
 extern "C" {
@@ -431,61 +500,10 @@ int cz_plan_segments(const cz_frame_desc *h_desc, uint32_t count, int open, uint
         return fail(CZ_EINVAL, "cz_plan_segments: null pointer");
     if (seg_blocks < 2)
         return fail(CZ_EINVAL, "cz_plan_segments: seg_blocks must be >= 2");
-    const uint32_t split_above = seg_blocks + seg_blocks / 2;
     std::vector<cz_segment> segs;
     std::vector<cz_combine> combs;
-    segs.reserve(count);
     uint32_t parts = 0;
-    for (uint32_t i = 0; i < count; i++) {
-        const uint64_t mlen = open ? (uint64_t)h_desc[i].len : (uint64_t)h_desc[i].len + CZ_MESSAGE_OVERHEAD;
-        uint32_t nblk = (uint32_t)((mlen + 63) / 64);
-        if (nblk == 0)
-            nblk = 1;
-        if (nblk <= split_above) {
-            segs.push_back({i, 0u, nblk, 0xffffffffu});
-            continue;
-        }
-        // Seal segment s covers box blocks [s*seg, (s+1)*seg).  Open segments s >= 1 start one
-        // block later, at s*seg + 1, so each one's payload chunks start at s*seg: the 33-byte
-        // shift puts payload chunk g across box blocks g and g+1.  Last segment: the remainder.
-        const uint32_t lead = open ? 1u : 0u;
-        const uint32_t ns = (nblk - lead + seg_blocks - 1) / seg_blocks;
-        combs.push_back({i, parts, ns, 0u});
-        for (uint32_t s = 0; s < ns; s++) {
-            const uint32_t b0 = s ? s * seg_blocks + lead : 0u;
-            const uint32_t b1 = s + 1 < ns ? (s + 1) * seg_blocks + lead : nblk;
-            segs.push_back({i, b0, b1 - b0, parts + s});
-        }
-        parts += ns;
-    }
-    // longest first, keyed on the kernel's loop count (output chunks), so that waves hold
-    // equal-length segments and can take the line-staged store path
-    auto chunks = [&](const cz_segment &g) -> uint32_t {
-        if (!open)
-            return g.nblocks;
-        const uint32_t len = h_desc[g.frame].len;
-        if (len < CZ_MESSAGE_OVERHEAD)
-            return 0u;
-        const uint32_t nblk = (len + 63) / 64, bend = g.first_block + g.nblocks;
-        const uint32_t cb = g.first_block ? g.first_block - 1 : 0u;
-        const uint32_t ce = bend == nblk ? (len - CZ_MESSAGE_OVERHEAD + 63) / 64 : bend - 1;
-        return ce - cb;
-    };
-    // Seal, within one length: segments whose input starts on a 128-byte line first, then the
-    // ones starting 64 bytes into a line, so that waves hold one line phase and the odd ones
-    // can read whole lines (seal_segment in cz_kernels.hip).  Key: chunks * 2 + (1 - phase).
-    auto phase = [&](const cz_segment &g) -> uint32_t {
-        return open ? 0u : (uint32_t)(((h_desc[g.frame].in_off + 64ull * g.first_block) >> 6) & 1u);
-    };
-    std::vector<std::pair<uint64_t, uint32_t>> key(segs.size());
-    for (size_t k = 0; k < segs.size(); k++)
-        key[k] = {2ull * chunks(segs[k]) + (1u - phase(segs[k])), (uint32_t)k};
-    std::stable_sort(key.begin(), key.end(), [](const std::pair<uint64_t, uint32_t> &a,
-                                                 const std::pair<uint64_t, uint32_t> &b) { return a.first > b.first; });
-    std::vector<cz_segment> sorted(segs.size());
-    for (size_t k = 0; k < segs.size(); k++)
-        sorted[k] = segs[key[k].second];
-    segs.swap(sorted);
+    plan_segments(h_desc, count, open, seg_blocks, segs, combs, parts);
     *nseg = (uint32_t)segs.size();
     *ncomb = (uint32_t)combs.size();
     *npart = parts;
@@ -569,11 +587,15 @@ void cz_ctx_destroy(cz_ctx *c)
     c->keys.release();
     c->subkeys.release();
     c->hdesc.release();
-    for (int k = 0; k < cz_ctx::PIPE; k++) {
+    for (int k = 0; k < cz_ctx::PIPE; k++)
         if (c->ps[k]) {
             (void)hipStreamSynchronize(c->ps[k]);
             (void)hipStreamDestroy(c->ps[k]);
         }
+    for (int k = 0; k < cz_ctx::NB; k++) {
+        for (hipEvent_t ev : {c->ev_in[k], c->ev_kern[k], c->ev_out[k]})
+            if (ev)
+                (void)hipEventDestroy(ev);
         c->pin[k].release();
         c->pout[k].release();
         c->pflags[k].release();
@@ -673,9 +695,13 @@ int cz_ctx_open(cz_ctx *c, const cz_frame_desc *h_desc, uint32_t count, const vo
     return ctx_run(c, h_desc, count, h_in, in_bytes, h_out, out_bytes, h_status, false);
 }
 
-// Pipelined host-staged uniform batch: chunk k of `chunk` frames runs
-// H2D -> kernel -> D2H on stream k % PIPE with that stream's buffers, so PCIe
-// transfers in both directions overlap each other and the kernels.
+// Pipelined host-staged uniform batch.  Chunk k of `chunk` frames uses buffer set k % NB:
+//   stream 0: H2D of chunk k (after the kernel of chunk k - NB released the set's input)
+//   stream 1: kernel of chunk k (after its H2D, and after the D2H of chunk k - NB released the
+//             set's output)
+//   stream 2: D2H of chunk k (after its kernel)
+// One stream per direction keeps each DMA direction's queue in chunk order, so H2D and D2H run
+// concurrently (full duplex) instead of queueing behind each other on shared streams.
 static int ctx_uniform(cz_ctx *c, bool seal, uint32_t count, uint32_t len, const void *h_in, uint64_t in_stride,
                        void *h_out, uint64_t out_stride, uint64_t counter0, const uint8_t *h_flags8,
                        uint16_t *h_status, int check, uint32_t chunk)
@@ -696,9 +722,13 @@ static int ctx_uniform(cz_ctx *c, bool seal, uint32_t count, uint32_t len, const
     hipError_t e;
     (void)hipSetDevice(c->device);
     const uint32_t per = chunk < count ? chunk : count;
-    for (int k = 0; k < cz_ctx::PIPE; k++) {
+    for (int k = 0; k < cz_ctx::PIPE; k++)
         if (!c->ps[k] && (e = hipStreamCreateWithFlags(&c->ps[k], hipStreamNonBlocking)) != hipSuccess)
             return hip_fail(e, "hipStreamCreate");
+    for (int k = 0; k < cz_ctx::NB; k++) {
+        for (hipEvent_t *ev : {&c->ev_in[k], &c->ev_kern[k], &c->ev_out[k]})
+            if (!*ev && (e = hipEventCreateWithFlags(ev, hipEventDisableTiming)) != hipSuccess)
+                return hip_fail(e, "hipEventCreate");
         if ((e = c->pin[k].reserve((uint64_t)per * in_stride + 16)) != hipSuccess ||
             (e = c->pout[k].reserve((uint64_t)per * out_stride + 16)) != hipSuccess ||
             (e = c->pflags[k].reserve(per)) != hipSuccess || (e = c->pstatus[k].reserve(2ull * per)) != hipSuccess)
@@ -706,24 +736,30 @@ static int ctx_uniform(cz_ctx *c, bool seal, uint32_t count, uint32_t len, const
     }
     const uint8_t *hin = (const uint8_t *)h_in;
     uint8_t *hout = (uint8_t *)h_out;
+    hipStream_t s_in = c->ps[0], s_k = c->ps[1], s_out = c->ps[2];
     uint32_t k = 0;
     for (uint32_t f0 = 0; f0 < count; f0 += per, k++) {
         const uint32_t nc = count - f0 < per ? count - f0 : per;
-        const int q = k % cz_ctx::PIPE;
-        hipStream_t st = c->ps[q];
+        const int q = k % cz_ctx::NB;
+        const bool reuse = k >= (uint32_t)cz_ctx::NB;
         const uint64_t ib = (uint64_t)(nc - 1) * in_stride + len;
-        if ((e = hipMemcpyAsync(c->pin[q].ptr, hin + (uint64_t)f0 * in_stride, ib, hipMemcpyHostToDevice, st)) !=
-            hipSuccess)
+        if ((reuse && (e = hipStreamWaitEvent(s_in, c->ev_kern[q], 0)) != hipSuccess) ||
+            (e = hipMemcpyAsync(c->pin[q].ptr, hin + (uint64_t)f0 * in_stride, ib, hipMemcpyHostToDevice, s_in)) !=
+                hipSuccess)
             return hip_fail(e, "H2D");
+        const uint8_t *dfl = nullptr;
+        if (seal && h_flags8) {
+            if ((e = hipMemcpyAsync(c->pflags[q].ptr, h_flags8 + f0, nc, hipMemcpyHostToDevice, s_in)) != hipSuccess)
+                return hip_fail(e, "H2D flags");
+            dfl = (const uint8_t *)c->pflags[q].ptr;
+        }
+        if ((e = hipEventRecord(c->ev_in[q], s_in)) != hipSuccess ||
+            (e = hipStreamWaitEvent(s_k, c->ev_in[q], 0)) != hipSuccess ||
+            (reuse && (e = hipStreamWaitEvent(s_k, c->ev_out[q], 0)) != hipSuccess))
+            return hip_fail(e, "event");
         if (seal) {
-            const uint8_t *dfl = nullptr;
-            if (h_flags8) {
-                if ((e = hipMemcpyAsync(c->pflags[q].ptr, h_flags8 + f0, nc, hipMemcpyHostToDevice, st)) != hipSuccess)
-                    return hip_fail(e, "H2D flags");
-                dfl = (const uint8_t *)c->pflags[q].ptr;
-            }
             e = czk_seal_uniform(c->pin[q].ptr, in_stride, c->pout[q].ptr, out_stride, nc, len, c->subkeys.ptr,
-                                 counter0 + f0, dfl, st);
+                                 counter0 + f0, dfl, s_k);
         } else {
             // the chunk's first frame must beat the previous chunk's last nonce: read it from the host copy
             uint64_t floor0 = counter0;
@@ -734,16 +770,21 @@ static int ctx_uniform(cz_ctx *c, bool seal, uint32_t count, uint32_t len, const
                     floor0 = (floor0 << 8) | pb[b];
             }
             e = czk_open_uniform(c->pin[q].ptr, in_stride, c->pout[q].ptr, out_stride, nc, len, c->subkeys.ptr, floor0,
-                                 check, (uint16_t *)c->pstatus[q].ptr, st);
+                                 check, (uint16_t *)c->pstatus[q].ptr, s_k);
         }
         if (e != hipSuccess)
             return hip_fail(e, "launch");
+        if ((e = hipEventRecord(c->ev_kern[q], s_k)) != hipSuccess ||
+            (e = hipStreamWaitEvent(s_out, c->ev_kern[q], 0)) != hipSuccess)
+            return hip_fail(e, "event");
         if ((e = hipMemcpyAsync(hout + (uint64_t)f0 * out_stride, c->pout[q].ptr, (uint64_t)nc * out_stride,
-                                hipMemcpyDeviceToHost, st)) != hipSuccess)
+                                hipMemcpyDeviceToHost, s_out)) != hipSuccess)
             return hip_fail(e, "D2H");
-        if (!seal && (e = hipMemcpyAsync(h_status + f0, c->pstatus[q].ptr, 2ull * nc, hipMemcpyDeviceToHost, st)) !=
+        if (!seal && (e = hipMemcpyAsync(h_status + f0, c->pstatus[q].ptr, 2ull * nc, hipMemcpyDeviceToHost, s_out)) !=
                          hipSuccess)
             return hip_fail(e, "D2H status");
+        if ((e = hipEventRecord(c->ev_out[q], s_out)) != hipSuccess)
+            return hip_fail(e, "event");
     }
     for (int q = 0; q < cz_ctx::PIPE; q++)
         if ((e = hipStreamSynchronize(c->ps[q])) != hipSuccess)

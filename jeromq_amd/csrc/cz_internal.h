@@ -4,6 +4,8 @@
 #include <stdarg.h>
 #include <stdint.h>
 
+#include <vector>
+
 #include "../../include/curvezmq_mi355x.h"
 
 extern "C" {
@@ -24,6 +26,27 @@ namespace czi {
 int fail(int code, const char *fmt, ...);
 int hip_fail(hipError_t e, const char *where);
 const uint8_t *prefix_for(int direction);
+void plan_segments(const cz_frame_desc *h_desc, uint32_t count, int open, uint32_t seg_blocks,
+                   std::vector<cz_segment> &segs, std::vector<cz_combine> &combs, uint32_t &npart);
+
+// segments, combine records and partial records the planner makes for one frame of `len` (payload for seal, body
+// for open) -- lets a caller size its buffers before planning
+inline void plan_counts(uint64_t len, int open, uint32_t seg_blocks, uint64_t &nseg, uint64_t &ncomb, uint64_t &npart)
+{
+    const uint64_t mlen = open ? len : len + CZ_MESSAGE_OVERHEAD;
+    uint64_t nblk = (mlen + 63) / 64;
+    if (nblk == 0)
+        nblk = 1;
+    if (nblk <= seg_blocks + seg_blocks / 2) {
+        nseg += 1;
+        return;
+    }
+    const uint64_t lead = open ? 1u : 0u;
+    const uint64_t ns = (nblk - lead + seg_blocks - 1) / seg_blocks;
+    nseg += ns;
+    npart += ns;
+    ncomb += 1;
+}
 
 // device buffer that grows on demand (never shrinks)
 struct DevBuf {

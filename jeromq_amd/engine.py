@@ -15,6 +15,10 @@ import ctypes
 from . import _lib
 
 
+class _IOVEC(ctypes.Structure):
+    _fields_ = [("base", ctypes.c_void_p), ("len", ctypes.c_uint64)]
+
+
 class CurveBatchEngine:
     def __init__(self, arena_bytes=1 << 26, device=0):
         self._L = _lib.lib()
@@ -75,6 +79,14 @@ class CurveBatchEngine:
         p, n = ctypes.c_void_p(), ctypes.c_uint64()
         _lib.check(self._L.cz_engine_wire_out(self._h, conn, ctypes.byref(p), ctypes.byref(n)), "cz_engine_wire_out")
         return ctypes.string_at(p.value, n.value) if n.value else b""
+
+    def wire_iov(self, conn):
+        """The connection's stream as gather-write pieces [(address, length)] of the flush output."""
+        cnt = ctypes.c_uint32()
+        _lib.check(self._L.cz_engine_wire_iov(self._h, conn, None, 0, ctypes.byref(cnt)), "cz_engine_wire_iov")
+        arr = (_IOVEC * max(cnt.value, 1))()
+        _lib.check(self._L.cz_engine_wire_iov(self._h, conn, arr, cnt.value, ctypes.byref(cnt)), "cz_engine_wire_iov")
+        return [(arr[k].base, arr[k].len) for k in range(cnt.value)]
 
     def recv(self, conn, wire):
         b = bytes(wire)

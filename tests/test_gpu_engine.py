@@ -226,3 +226,50 @@ def test_engine_zero_copy_receive_from_socket(torch_dev, L):
         a.close()
         b.close()
     assert srv.error(s) == (0, 0) and got == msgs
+
+
+def test_engine_pipelined_flush_out_and_iov(torch_dev, L):
+    """A flush of tens of MiB runs as several pipelined groups (~8 MiB+ each: H2D of one group
+    overlapping the seal + D2H of the one before).  Sends interleave across connections and payloads are allocated in the
+    arena out of send order, so a group's arena range reaches past its own messages.  Each
+    connection's stream, gathered (wire_out) or as writev pieces (wire_iov), equals the
+    V2-framed oracle seal of its messages in its own send order."""
+    from jeromq_amd.engine import CurveBatchEngine
+    rng = np.random.default_rng(11)
+    ncon = 6
+    cli = CurveBatchEngine(arena_bytes=128 << 20)
+    cc = [cli.add_connection(_precom(i)) for i in range(ncon)]
+    sizes = {i: [int(s) for s in rng.choice([0, 33, 1000, 4096, 65536, 262144, 1 << 20], size=24, p=[.1, .1, .1, .1, .2, .2, .2])]
+             for i in range(ncon)}
+    sent = {i: [(splitmix_bytes(s, 900 + 50 * i + k), k & 3) for k, s in enumerate(sizes[i])] for i in range(ncon)}
+    # connection 0 queues all its messages together (one piece); the others interleave
+    order = [(0, k) for k in range(24)]
+    rest = [(i, k) for i in range(1, ncon) for k in range(24)]
+    rest.sort(key=lambda t: (t[1], rng.random()))
+    order += rest
+    # allocate every arena buffer first, in reverse send order for the interleaved part
+    bufs = {}
+    for i, k in order[:24] + order[24:][::-1]:
+        p = sent[i][k][0]
+        bufs[(i, k)] = cli.msg_alloc(len(p)) if p else None
+        if p:
+            bufs[(i, k)][:] = p
+    for i, k in order:
+        p, fl = sent[i][k]
+        payload = bufs[(i, k)] if p else b""
+        assert cli.send(cc[i], payload, more=bool(fl & 1), command=bool(fl & 2)) == 0
+    cli.flush_out()
+    for i in range(ncon):
+        want = _oracle_wire(sent[i], _precom(i), 0, 3)
+        assert cli.wire_out(cc[i]) == want, f"connection {i}"
+        pieces = cli.wire_iov(cc[i])
+        assert b"".join(ctypes.string_at(a, n) for a, n in pieces) == want
+        if i == 0:
+            assert len(pieces) == 1
+        else:
+            assert len(pieces) > 1
+    # a second, small flush on the same engine (one group) still chains the nonces
+    cli.send(cc[1], b"after")
+    cli.flush_out()
+    assert cli.wire_out(cc[1]) == v2_encode(or_curve_encode(b"after", 0, 3 + 24, 0, _precom(1)))
+    assert cli.wire_out(cc[2]) == b"" and cli.wire_iov(cc[2]) == []

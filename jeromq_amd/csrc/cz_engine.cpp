@@ -25,6 +25,7 @@
 
 #include <algorithm>
 #include <chrono>
+#include <thread>
 #include <vector>
 
 #include "cz_internal.h"
@@ -399,9 +400,7 @@ struct cz_engine {
         in_msgs.clear();
         for (Conn &c : conns)
             c.in_msgs.clear();
-        // 0. the live connections' received bytes, in groups of ~equal bytes.  Each group's H2D
-        //    (whole receive buffers, DMA'd straight from the pinned per-connection buffers) is
-        //    issued before any parsing, so the copies run while the host parses and plans.
+        // 0. the live connections, in groups of ~equal received bytes
         struct Parsed {
             uint32_t conn;
             uint32_t first, count;  // range in frames
@@ -415,7 +414,7 @@ struct cz_engine {
             Conn &c = conns[ci];
             if (c.error || c.rx_len == 0)
                 continue;
-            parsed.push_back({(uint32_t)ci, 0u, 0u, rx_total, 0u, 0});
+            parsed.push_back({(uint32_t)ci, 0u, 0u, 0u, 0u, 0});
             rx_total += c.rx_len;
         }
         struct Group {
@@ -437,17 +436,31 @@ struct cz_engine {
             }
         }
         hipError_t e;
-        std::vector<hipEvent_t> ev(groups.size(), nullptr), evm(groups.size(), nullptr), evk(groups.size(), nullptr);
-        EvGuard evguard{ev}, evmguard{evm}, evkguard{evk};
+        std::vector<hipEvent_t> evm(groups.size(), nullptr), evk(groups.size(), nullptr);
+        EvGuard evmguard{evm}, evkguard{evk};
         for (size_t gi = 0; gi < groups.size(); gi++)
-            if ((e = hipEventCreateWithFlags(&ev[gi], hipEventDisableTiming)) != hipSuccess ||
-                (e = hipEventCreateWithFlags(&evm[gi], hipEventDisableTiming)) != hipSuccess ||
+            if ((e = hipEventCreateWithFlags(&evm[gi], hipEventDisableTiming)) != hipSuccess ||
                 (e = hipEventCreateWithFlags(&evk[gi], hipEventDisableTiming)) != hipSuccess)
                 return hip_fail(e, "hipEventCreate");
-        // ps[0]: received bytes H2D; stream: metadata H2D; ps[1]: kernels; ps[2]: D2H
+        // ps[0]: received bytes H2D, one DMA per connection straight from its pinned receive buffer,
+        // every group issued before any parsing so the copies run while the host parses and plans;
+        // `stream`: metadata H2D; ps[1]: unpack + open; ps[2]: D2H.  (A gather kernel reading the
+        // receive buffers over PCIe instead of the per-connection DMAs measured slower.)
         hipStream_t qh = ps[0], qk = ps[1], qo = ps[2], qm = stream;
-        if (rx_total && (e = d_wire.reserve(rx_total)) != hipSuccess)
-            return hip_fail(e, "cz_engine: alloc");
+        std::vector<hipEvent_t> ev(groups.size(), nullptr);
+        EvGuard evguard{ev};
+        for (size_t gi = 0; gi < groups.size(); gi++)
+            if ((e = hipEventCreateWithFlags(&ev[gi], hipEventDisableTiming)) != hipSuccess)
+                return hip_fail(e, "hipEventCreate");
+        {
+            uint64_t off = 0;
+            for (Parsed &p : parsed) {
+                p.rx_off = off;
+                off += conns[p.conn].rx_len;
+            }
+            if (off && (e = d_wire.reserve(off)) != hipSuccess)
+                return hip_fail(e, "cz_engine: alloc");
+        }
         for (size_t gi = 0; gi < groups.size(); gi++) {
             for (size_t pi = groups[gi].pa; pi < groups[gi].pb; pi++) {
                 const Parsed &p = parsed[pi];
@@ -459,77 +472,115 @@ struct cz_engine {
                 return hip_fail(e, "cz_engine: H2D");
         }
         pt.mark("h2d-issue");
-        // 1. parse every connection's whole frames (V2Decoder); a partial frame waits for more bytes
-        std::vector<cz_v2_frame> frames;
-        for (Parsed &p : parsed) {
-            const Conn &c = conns[p.conn];
-            // parse in chunks of CH frames (a frame is >= 2 bytes, so sizing by bytes would cost 8x the data)
-            constexpr uint32_t CH = 4096;
-            const size_t base = frames.size();
-            uint64_t consumed = 0;
-            int prc = CZ_OK;
-            for (;;) {
-                const size_t at = frames.size();
-                frames.resize(at + CH);
-                uint32_t nf = 0;
-                uint64_t used = 0;
-                prc = cz_v2_parse((const uint8_t *)c.rx.ptr + consumed, c.rx_len - consumed, -1, frames.data() + at,
-                                  CH, &nf, &used);
-                frames.resize(at + nf);
-                for (uint32_t k = 0; k < nf; k++)
-                    frames[at + k].body_off += consumed;
-                consumed += used;
-                if (prc != CZ_OK || nf < CH)
-                    break;
+        // 1. per group, on its own host thread: parse each connection's whole frames (V2Decoder; a
+        //    partial frame waits for more bytes), build the group's descriptors -- bodies unpacked
+        //    into aligned slots, each connection's frames chained by prev (group-relative
+        //    indices) -- and plan its segments.  Offsets are group-relative until step 2.
+        struct GroupWork {
+            std::vector<cz_v2_frame> frames;
+            std::vector<cz_frame_desc> desc;
+            std::vector<cz_v2_item> items;
+            Segs sg;
+            uint64_t bslot = 0, pslot = 0;
+        };
+        std::vector<GroupWork> gw(groups.size());
+        auto work = [&](size_t gi) {
+            GroupWork &w = gw[gi];
+            const Group &g = groups[gi];
+            constexpr uint32_t CH = 4096;  // parse in chunks of CH frames
+            for (size_t q = g.pa; q < g.pb; q++) {
+                Parsed &p = parsed[q];
+                const Conn &c = conns[p.conn];
+                const size_t base = w.frames.size();
+                uint64_t consumed = 0;
+                int prc = CZ_OK;
+                for (;;) {
+                    const size_t at = w.frames.size();
+                    w.frames.resize(at + CH);
+                    uint32_t nf = 0;
+                    uint64_t used = 0;
+                    prc = cz_v2_parse((const uint8_t *)c.rx.ptr + consumed, c.rx_len - consumed, -1,
+                                      w.frames.data() + at, CH, &nf, &used);
+                    w.frames.resize(at + nf);
+                    for (uint32_t k = 0; k < nf; k++)
+                        w.frames[at + k].body_off += consumed;
+                    consumed += used;
+                    if (prc != CZ_OK || nf < CH)
+                        break;
+                }
+                p.first = (uint32_t)base;  // group-relative until step 2
+                p.count = (uint32_t)(w.frames.size() - base);
+                p.consumed = consumed;
+                p.perr = prc == CZ_OK ? 0 : prc;
             }
-            p.first = (uint32_t)base;
-            p.count = (uint32_t)(frames.size() - base);
-            p.consumed = consumed;
-            p.perr = prc == CZ_OK ? 0 : prc;
-        }
-        const uint32_t n = (uint32_t)frames.size();
-        pt.mark("parse");
-        // 2. descriptors: bodies unpacked into aligned slots, each connection's frames chained by
-        //    prev (group-relative indices)
-        std::vector<cz_frame_desc> desc(n);
-        std::vector<cz_v2_item> items(n);
-        uint64_t bslot = 0, pslot = 0;
-        for (Group &g : groups) {
-            g.fa = parsed[g.pa].first;
-            g.pl0 = pslot;
+            const size_t gn = w.frames.size();
+            w.desc.resize(gn);
+            w.items.resize(gn);
             for (size_t q = g.pa; q < g.pb; q++) {
                 const Parsed &p = parsed[q];
                 const Conn &c = conns[p.conn];
                 for (uint32_t k = 0; k < p.count; k++) {
                     const uint32_t i = p.first + k;
-                    const cz_v2_frame &f = frames[i];
+                    const cz_v2_frame &f = w.frames[i];
                     const uint64_t plen = f.size > CZ_MESSAGE_OVERHEAD ? f.size - CZ_MESSAGE_OVERHEAD : 0;
-                    items[i] = {p.rx_off + f.body_off, bslot, f.size, 0u};
-                    desc[i] = {bslot, pslot, f.size, c.rx_key, c.peer_nonce, CZ_DESC_CHECK_NONCE,
-                               k ? (int32_t)(i - 1 - g.fa) : -1};
-                    bslot += round_up(std::max<uint64_t>(f.size, 1), SLOT_ALIGN);
-                    pslot += round_up(std::max<uint64_t>(plen, 1), SLOT_ALIGN);
+                    w.items[i] = {p.rx_off + f.body_off, w.bslot, f.size, 0u};
+                    w.desc[i] = {w.bslot, w.pslot, f.size, c.rx_key, c.peer_nonce, CZ_DESC_CHECK_NONCE,
+                                 k ? (int32_t)(i - 1) : -1};
+                    w.bslot += round_up(std::max<uint64_t>(f.size, 1), SLOT_ALIGN);
+                    w.pslot += round_up(std::max<uint64_t>(plen, 1), SLOT_ALIGN);
                 }
             }
-            g.fb = parsed[g.pb - 1].first + parsed[g.pb - 1].count;
+            // the planner reads only lengths for open (no line phase), so relative offsets do
+            plan_segments(w.desc.data(), (uint32_t)gn, 1, SEG_BLOCKS, w.sg.seg, w.sg.comb, w.sg.npart);
+            w.sg.nseg = (uint32_t)w.sg.seg.size();
+            w.sg.ncomb = (uint32_t)w.sg.comb.size();
+        };
+        {
+            std::vector<std::thread> th;
+            for (size_t gi = 1; gi < groups.size(); gi++)
+                th.emplace_back(work, gi);
+            if (!groups.empty())
+                work(0);
+            for (std::thread &t : th)
+                t.join();
+        }
+        pt.mark("parse+desc+plan");
+        // 2. concatenate the groups: absolute frame indices and slot offsets
+        uint32_t n = 0;
+        uint64_t bslot = 0, pslot = 0;
+        for (size_t gi = 0; gi < groups.size(); gi++) {
+            Group &g = groups[gi];
+            g.fa = n;
+            for (size_t q = g.pa; q < g.pb; q++)
+                parsed[q].first += n;
+            n += (uint32_t)gw[gi].frames.size();
+            g.fb = n;
+            g.pl0 = pslot;
+            for (cz_frame_desc &d : gw[gi].desc) {
+                d.in_off += bslot;
+                d.out_off += pslot;
+            }
+            for (cz_v2_item &it : gw[gi].items)
+                it.dst_off += bslot;
+            bslot += gw[gi].bslot;
+            pslot += gw[gi].pslot;
             g.pl1 = pslot;
         }
+        std::vector<cz_frame_desc> desc;
+        desc.reserve(n);
+        for (const GroupWork &w : gw)
+            desc.insert(desc.end(), w.desc.begin(), w.desc.end());
         if (n) {
-            // plans per group; device segment / combine / work arrays hold all groups at once
-            std::vector<Segs> gs(groups.size());
+            // device segment / combine / work arrays hold all groups at once
             uint64_t nseg = 0, ncomb = 0, npart = 0;
             std::vector<uint64_t> soff(groups.size()), coff(groups.size()), woff(groups.size());
             for (size_t gi = 0; gi < groups.size(); gi++) {
-                const Group &g = groups[gi];
-                plan_segments(desc.data() + g.fa, g.fb - g.fa, 1, SEG_BLOCKS, gs[gi].seg, gs[gi].comb, gs[gi].npart);
-                gs[gi].nseg = (uint32_t)gs[gi].seg.size();
-                gs[gi].ncomb = (uint32_t)gs[gi].comb.size();
                 soff[gi] = nseg;
                 coff[gi] = ncomb;
                 woff[gi] = npart;
-                nseg += gs[gi].nseg;
-                ncomb += gs[gi].ncomb;
-                npart += gs[gi].npart;
+                nseg += gw[gi].sg.nseg;
+                ncomb += gw[gi].sg.ncomb;
+                npart += gw[gi].sg.npart;
             }
             const uint64_t m_items = 0, m_desc = (uint64_t)n * sizeof(cz_v2_item),
                            m_seg = m_desc + (uint64_t)n * sizeof(cz_frame_desc),
@@ -549,13 +600,15 @@ struct cz_engine {
                 return hip_fail(e, "cz_engine: alloc");
             // pinned copies of the host-built arrays: pageable sources would make each H2D synchronous
             uint8_t *hm = (uint8_t *)h_meta.ptr;
-            memcpy(hm + m_items, items.data(), (uint64_t)n * sizeof(cz_v2_item));
             memcpy(hm + m_desc, desc.data(), (uint64_t)n * sizeof(cz_frame_desc));
             for (size_t gi = 0; gi < groups.size(); gi++) {
-                memcpy(hm + m_seg + soff[gi] * sizeof(cz_segment), gs[gi].seg.data(),
-                       (uint64_t)gs[gi].nseg * sizeof(cz_segment));
-                memcpy(hm + m_comb + coff[gi] * sizeof(cz_combine), gs[gi].comb.data(),
-                       (uint64_t)gs[gi].ncomb * sizeof(cz_combine));
+                const GroupWork &w = gw[gi];
+                memcpy(hm + m_items + groups[gi].fa * sizeof(cz_v2_item), w.items.data(),
+                       w.items.size() * sizeof(cz_v2_item));
+                memcpy(hm + m_seg + soff[gi] * sizeof(cz_segment), w.sg.seg.data(),
+                       (uint64_t)w.sg.nseg * sizeof(cz_segment));
+                memcpy(hm + m_comb + coff[gi] * sizeof(cz_combine), w.sg.comb.data(),
+                       (uint64_t)w.sg.ncomb * sizeof(cz_combine));
             }
             const cz_v2_item *h_items = (const cz_v2_item *)(hm + m_items);
             const cz_frame_desc *h_desc = (const cz_frame_desc *)(hm + m_desc);
@@ -567,7 +620,7 @@ struct cz_engine {
                 const uint32_t gn = g.fb - g.fa;
                 if (gn == 0)
                     continue;
-                const Segs &sg = gs[gi];
+                const Segs &sg = gw[gi].sg;
                 cz_frame_desc *dd = (cz_frame_desc *)d_desc.ptr + g.fa;
                 cz_segment *dsg = (cz_segment *)d_seg.ptr + soff[gi];
                 cz_combine *dcb = (cz_combine *)d_comb.ptr + coff[gi];

@@ -314,9 +314,17 @@ struct EmitLines {
         const u32 r = lane >> 3;
 #ifdef CZ_DIAG_L2STORE
         uint8_t *p = wbase + 128u * r + 16u * c;  // every line of the wave onto its first 8 KiB
-        const u64 step = 1024u;
+        const u64 step = 1024u;  // (diagnostic build: plain stores)
 #else
-        uint8_t *p = wbase + (u64)r * stride + 128ull * line + 16u * c;
+        // wave-uniform line base in SGPRs, advanced by the scalar unit, plus a per-lane 32-bit
+        // offset: saddr stores with no 64-bit VALU address arithmetic per store
+        const u64 wb = (u64)(uintptr_t)wbase;
+        // (readfirstlane returns int: each half goes through u32 before widening, or a low half
+        // with bit 31 set would sign-extend over the high one)
+        u64 p = (((u64)(u32)__builtin_amdgcn_readfirstlane((u32)(wb >> 32)) << 32) |
+                 (u64)(u32)__builtin_amdgcn_readfirstlane((u32)wb)) +
+                128ull * line;
+        const u32 voff = r * (u32)stride + 16u * c;
         const u64 step = 8ull * stride;
 #endif
 #ifdef CZ_DIAG_NOTAG
@@ -336,14 +344,18 @@ struct EmitLines {
 #else
             if (!skip)
 #endif
-#ifdef CZ_DIAG_STORE_POLICY  // cache-policy bits on the line stores, e.g. -DCZ_DIAG_STORE_POLICY='"sc1"'
+#ifndef CZ_DIAG_STORE_POLICY  // cache-policy bits on the line stores, e.g. -DCZ_DIAG_STORE_POLICY='"sc1"'
+#define CZ_DIAG_STORE_POLICY ""
+#endif
+#ifdef CZ_DIAG_L2STORE
+                *reinterpret_cast<uint4 *>(p) = v;
+#else
             {
                 typedef unsigned v4u __attribute__((ext_vector_type(4)));
                 const v4u d = {v.x, v.y, v.z, v.w};
-                asm volatile("global_store_dwordx4 %0, %1, off " CZ_DIAG_STORE_POLICY ::"v"(p), "v"(d) : "memory");
+                asm volatile("global_store_dwordx4 %0, %1, %2 " CZ_DIAG_STORE_POLICY ::"v"(voff), "v"(d), "s"(p)
+                             : "memory");
             }
-#else
-                *reinterpret_cast<uint4 *>(p) = v;
 #endif
             p += step;
         }
@@ -598,13 +610,11 @@ __device__ __forceinline__ void seal_frame(const uint8_t *__restrict__ in, u32 n
         }
         carry = L[7];
         if (nfull >= 2) {
-            zmq_full_block(1, L + 7);
-            u32 cy[9];
-#pragma unroll
-            for (int k = 0; k < 9; k++)
-                cy[k] = L[23 + k];
-            blk = 2;
-            for (u32 k = 1; 2u * k + 1u < nfull; k++) {
+            // Chunks 6 and 7 of a line (bytes 96..127) matter only as the carry of the next
+            // iteration; past the payload end they are not loaded and the registers keep stale,
+            // unused words (no zero fill: -8 v_mov per pair).  (Loading line k + 1 at the end of
+            // iteration k, ahead of the line stores, measured 2% slower.)
+            auto load_line = [&](u32 k) {
                 const uint8_t *src = in + 128u * k;
                 const u32 o = 128u * k;
 #pragma unroll
@@ -614,9 +624,20 @@ __device__ __forceinline__ void seal_frame(const uint8_t *__restrict__ in, u32 n
                 }
 #pragma unroll
                 for (int c = 6; c < 8; c++) {
-                    V4 v = ld16<AL>(src + 16 * c, inlen > o + 16u * c ? inlen - o - 16u * c : 0);
-                    L[4 * c] = v.x; L[4 * c + 1] = v.y; L[4 * c + 2] = v.z; L[4 * c + 3] = v.w;
+                    if (inlen > o + 16u * c) {
+                        V4 v = ld16f<AL>(src + 16 * c);
+                        L[4 * c] = v.x; L[4 * c + 1] = v.y; L[4 * c + 2] = v.z; L[4 * c + 3] = v.w;
+                    }
                 }
+            };
+            u32 cy[9];
+            zmq_full_block(1, L + 7);
+#pragma unroll
+            for (int q = 0; q < 9; q++)
+                cy[q] = L[23 + q];
+            blk = 2;
+            for (u32 k = 1; 2u * k + 1u < nfull; k++) {
+                load_line(k);
                 u32 W[17];
 #pragma unroll
                 for (int q = 0; q < 9; q++)
@@ -869,8 +890,11 @@ __device__ __forceinline__ u32 open_frame(const uint8_t *__restrict__ in, u32 si
         }
     }
 
-    // one block b >= 1 whose 64 ciphertext bytes are in C (full: all 64 valid)
-    auto open_block = [&](u32 blk, bool full) {
+    // one block b >= 1 whose 64 ciphertext bytes are in C (full: all 64 valid).  drain: every
+    // load in flight has landed by now (the block's keystream and MAC took ~1000 VALU); say so
+    // before the emit, whose line flush issues stores -- vmcnt counts stores too, so otherwise
+    // the next block's first use of the pair's second half waits for those stores to complete.
+    auto open_block = [&](u32 blk, bool full, bool drain = false) {
         ksblock(x, blk, 0u);
         if (full) {
             poly_block(P, C[0], C[1], C[2], C[3], 1u);
@@ -901,6 +925,8 @@ __device__ __forceinline__ u32 open_frame(const uint8_t *__restrict__ in, u32 si
 #pragma unroll
             for (int t = 0; t < 16; t++)
                 O[t] = funnel(E[t + 1], E[t], 1);
+            if (drain)
+                __builtin_amdgcn_s_waitcnt(0x0f70);  // vmcnt(0), expcnt / lgkmcnt unchanged (gfx9 encoding)
             emit_open(blk - 1, O, full);
 #pragma unroll
             for (int k = 0; k < 8; k++)
@@ -936,7 +962,7 @@ __device__ __forceinline__ u32 open_frame(const uint8_t *__restrict__ in, u32 si
 #pragma unroll
                 for (int q = 0; q < 16; q++)
                     C[q] = M[q];
-                open_block(2u * k, true);
+                open_block(2u * k, true, true);
 #pragma unroll
                 for (int q = 0; q < 16; q++)
                     C[q] = M[16 + q];

@@ -269,10 +269,26 @@ def cpu_baseline(wl, target_s):
     gibs = count * n / dt / 2**30
     # the GPU box's CPU share is 16 cores: the same sample on 16 threads, reported beside it
     dt16 = run(count, 16)
-    return {"value": round(gibs, 4), "unit": "GiB/s", "cores": 1, "kind": "port",
-            "value_16_threads": round(count * n / dt16 / 2**30, 4),
-            "sample": f"{count} x {n} B frames sealed by oracle/curve_oracle.c (1 thread, {dt:.1f} s), "
-                      f"{os.cpu_count()} logical CPUs visible"}
+    res = {"value": round(gibs, 4), "unit": "GiB/s", "cores": 1, "kind": "port",
+           "value_16_threads": round(count * n / dt16 / 2**30, 4),
+           "sample": f"{count} x {n} B frames sealed by oracle/curve_oracle.c (1 thread, {dt:.1f} s), "
+                     f"{os.cpu_count()} logical CPUs visible"}
+    # an optimised CPU NaCl beside the scalar port: libsodium's crypto_box_afternm of the same
+    # box length (0^32 || flags || payload), 1 thread, ~2 s
+    sod = _libsodium()
+    if sod is not None:
+        mlen = n + 33
+        m = ctypes.create_string_buffer(mlen)
+        c = ctypes.create_string_buffer(mlen)
+        nonce = ctypes.create_string_buffer(b"CurveZMQMESSAGEC" + (3).to_bytes(8, "big"), 24)
+        k = ctypes.create_string_buffer(PRECOM, 32)
+        reps, t0 = 0, time.perf_counter()
+        while time.perf_counter() - t0 < 2.0:
+            for _ in range(64):
+                sod.crypto_box_afternm(c, m, ctypes.c_ulonglong(mlen), nonce, k)
+            reps += 64
+        res["libsodium_1core_GiBps"] = round(reps * n / (time.perf_counter() - t0) / 2**30, 4)
+    return res
 
 
 def copy_ceiling(dev, nbytes=1 << 30, chunk=64 << 20, reps=5):

@@ -73,6 +73,12 @@ constexpr int BLOCK = 256;              // threads per workgroup (4 waves)
 #define CZ_SEG_LINES_WAVES_PER_EU 3
 #endif
 #define CZ_SEG_LINES_OCC __attribute__((amdgpu_waves_per_eu(CZ_SEG_LINES_WAVES_PER_EU, CZ_SEG_LINES_WAVES_PER_EU)))
+// k_open_segments: 3 waves per SIMD (left alone, the funnelled EmitShiftLines path took it to
+// 178 VGPRs, 2 waves)
+#ifndef CZ_OPEN_SEG_WAVES_PER_EU
+#define CZ_OPEN_SEG_WAVES_PER_EU 3
+#endif
+#define CZ_OPEN_SEG_OCC __attribute__((amdgpu_waves_per_eu(CZ_OPEN_SEG_WAVES_PER_EU, CZ_OPEN_SEG_WAVES_PER_EU)))
 #ifdef CZ_SEG_WAVES_PER_EU
 #define CZ_SEG_OCC __attribute__((amdgpu_waves_per_eu(CZ_SEG_WAVES_PER_EU, CZ_SEG_WAVES_PER_EU)))
 #else
@@ -1137,7 +1143,10 @@ __device__ void zero_bytes(uint8_t *p, u32 n)
 // lines written piecewise), so lines are ABSOLUTE: lane L's output [mine, mine + total)
 // starts d = mine & 127 bytes into its first line.  Its LDS row holds the line being built
 // (bytes [0, 128)) plus up to 64 bytes of the next; chunk q lands at (d + 64q) & 127 with
-// unaligned ds_write_b128, and completes a line when it reaches byte 128: at even q for
+// aligned LDS writes: b128 / b64 when every offset in the wave is a multiple of 16 / 8,
+// else 17 dwords of the chunk funnel-shifted by d & 3 bytes in registers (the dword
+// straddling two chunks completed by the next one; ds_write_b128 at byte offsets stalled the
+// LDS, SQ_LDS_UNALIGNED_STALL 18% of wave cycles), and completes a line when it reaches byte 128: at even q for
 // "class A" outputs (d >= 64), at odd q for the others.  The wave then stores that line of 8
 // outputs per global_store_dwordx4 (8 lanes x 16 bytes; each output's base and byte count
 // come from its owner lane by ds_bpermute) and each completing lane moves its row's bytes
@@ -1147,8 +1156,9 @@ __device__ void zero_bytes(uint8_t *p, u32 n)
 // -- its first and last, the tag slot -- are clipped to its bytes (st_range16): neighbouring
 // outputs own the other bytes.  emit/finish/close must be reached by all 64 lanes together:
 // ds_bpermute from an inactive lane returns garbage, not its base.
-constexpr u32 SROW = 208;  // 192 bytes used; 52 dwords apart: conflict-free 16-lane b128
+constexpr u32 SROW = 208;  // 16 headroom + 192 bytes used; 52 dwords apart: conflict-free 16-lane b128
 constexpr u32 SHIFT_LDS_BYTES = 64 * SROW;  // EmitShiftLines: 13 KiB per wave
+constexpr u32 SHEAD = 16;  // row bytes before line-space byte 0 (a chunk's first dword may start 4 early)
 struct EmitShiftLines {
     static constexpr bool cooperative = true;
     uint8_t *rows;   // this wave's 64 rows of SROW bytes
@@ -1156,11 +1166,18 @@ struct EmitShiftLines {
     u32 lane, total, last_q;
     u32 te;          // end of the output in its line space, d + total | bit 31: leave output bytes 16..31 to tag()
     u32 mixed;       // the wave holds outputs of both classes
+    u32 carry_w;     // the previous chunk's last dword (the first shifted dword of a chunk straddles both)
+    u32 walign;      // largest of 16 / 8 / 1 that divides every output's line offset in the wave
 
     // the launchers keep d + total below 2^31
     __device__ __forceinline__ void init(bool tag_slot)
     {
-        te = (((u32)(uintptr_t)mine & 127u) + total) | (tag_slot ? 0x80000000u : 0u);
+        carry_w = 0u;
+        const u32 d = (u32)(uintptr_t)mine & 127u;
+        walign = __builtin_amdgcn_ballot_w64((d & 15u) != 0u) == 0  ? 16u
+                 : __builtin_amdgcn_ballot_w64((d & 7u) != 0u) == 0 ? 8u
+                                                                     : 1u;
+        te = (d + total) | (tag_slot ? 0x80000000u : 0u);
         const uint64_t a = __builtin_amdgcn_ballot_w64((((u32)(uintptr_t)mine) & 64u) != 0u);
         mixed = (a != 0 && ~a != 0) ? 1u : 0u;
     }
@@ -1179,7 +1196,7 @@ struct EmitShiftLines {
 #pragma unroll
         for (u32 j = 0; j < 8; j++) {
             const u32 F = 8u * j + r;
-            const uint4 v = *reinterpret_cast<const uint4 *>(rows + F * SROW + 16u * c);
+            const uint4 v = *reinterpret_cast<const uint4 *>(rows + F * SROW + SHEAD + 16u * c);
             const int sel = (int)(F << 2);
             const u32 blo = (u32)__builtin_amdgcn_ds_bpermute(sel, (int)(u32)mb);
             const u32 bhi = (u32)__builtin_amdgcn_ds_bpermute(sel, (int)(u32)(mb >> 32));
@@ -1217,7 +1234,7 @@ struct EmitShiftLines {
     __device__ __forceinline__ void shift_row(u32 end)
     {
         asm volatile("" ::: "memory");
-        uint4 *row = reinterpret_cast<uint4 *>(rows + lane * SROW);
+        uint4 *row = reinterpret_cast<uint4 *>(rows + lane * SROW + SHEAD);
 #pragma unroll
         for (u32 u = 0; u < 4; u++)
             if (128u + 16u * u < end)
@@ -1228,10 +1245,31 @@ struct EmitShiftLines {
     {
         const u32 t = ((u32)(uintptr_t)mine & 127u) + 64u * q;
         const u32 pos = t & 127u;
-        uint8_t *w = rows + lane * SROW + pos;
+        // chunk byte i belongs at line-space byte pos + i.  With b = (4 - (pos & 3)) & 3, dword k of
+        // E = alignbyte(D[k], D[k-1], b) (D[-1] = the previous chunk's last dword) holds line-space
+        // bytes [pos - 4 + b + 4k, +4): every write is dword-aligned.  E[16] is this chunk's tail;
+        // the next chunk's E[0] rewrites that dword whole.
+        // A wave whose offsets are all 16- or 8-byte multiples writes the chunk as it is, with
+        // ds_write_b128 / b64 at aligned addresses (no funnel); only the other waves pay it.
+        const u32 b = (4u - (pos & 3u)) & 3u;
+        uint8_t *row0 = rows + lane * SROW + SHEAD;
+        if (walign == 16u) {
 #pragma unroll
-        for (u32 c = 0; c < 4; c++)
-            reinterpret_cast<U16ua *>(w + 16u * c)->v = make_uint4(D[4 * c], D[4 * c + 1], D[4 * c + 2], D[4 * c + 3]);
+            for (u32 c = 0; c < 4; c++)
+                reinterpret_cast<uint4 *>(row0 + pos)[c] = make_uint4(D[4 * c], D[4 * c + 1], D[4 * c + 2], D[4 * c + 3]);
+        } else if (walign == 8u) {
+#pragma unroll
+            for (u32 c = 0; c < 8; c++)
+                reinterpret_cast<uint2 *>(row0 + pos)[c] = make_uint2(D[2 * c], D[2 * c + 1]);
+        } else {
+            u32 *w = reinterpret_cast<u32 *>(row0 + pos + b - 4u);
+            w[0] = funnel(D[0], carry_w, b);
+#pragma unroll
+            for (u32 k = 1; k < 16; k++)
+                w[k] = funnel(D[k], D[k - 1], b);
+            w[16] = funnel(0u, D[15], b);
+            carry_w = D[15];
+        }
         const bool done = (t & 64u) != 0u;
         if (mixed) {
             flush<FL_MIXED>(q);
@@ -1241,8 +1279,8 @@ struct EmitShiftLines {
             last_q = q;
             return;
         }
-        if (__builtin_amdgcn_ballot_w64(done && pos + 64u > 128u) != 0 && done)
-            shift_row(pos + 64u);
+        if (__builtin_amdgcn_ballot_w64(done && pos + 64u + b > 128u) != 0 && done)
+            shift_row(pos + 64u + b);
         last_q = q;
     }
     __device__ __forceinline__ void emit_full(u32 q, const u32 D[16]) { emit(q, D); }
@@ -2133,7 +2171,7 @@ __global__ __launch_bounds__(BLOCK) void k_seal_combine(const cz_frame_desc *__r
         st16<false>(dst, tag[0], tag[1], tag[2], tag[3]);
 }
 
-__global__ __launch_bounds__(BLOCK) void k_open_segments(const cz_frame_desc *__restrict__ desc,
+__global__ __launch_bounds__(BLOCK) CZ_OPEN_SEG_OCC void k_open_segments(const cz_frame_desc *__restrict__ desc,
                                                           const cz_segment *__restrict__ segs, uint32_t nseg,
                                                           const uint8_t *__restrict__ in, uint8_t *__restrict__ out,
                                                           const uint8_t *__restrict__ subkeys,

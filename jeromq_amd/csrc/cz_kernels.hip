@@ -1193,6 +1193,25 @@ struct EmitShiftLines {
         const u32 r = lane >> 3;
         const u64 mb = (u64)(uintptr_t)mine;
         asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // the other lanes' ds_writes of this line
+        if constexpr (KIND == FL_PHASE) {
+            // Line k = q / 2 strictly inside every output of the wave (past the lines holding the
+            // tag slot, whole before the output's end): unclipped stores, only the base fetched.
+            const u32 k = q >> 1;
+            const bool inner = k >= 2u && 128u * (k + 1u) <= (te & 0x7fffffffu);
+            if (__builtin_amdgcn_ballot_w64(!inner) == 0) {
+#pragma unroll
+                for (u32 j = 0; j < 8; j++) {
+                    const u32 F = 8u * j + r;
+                    const uint4 v = *reinterpret_cast<const uint4 *>(rows + F * SROW + SHEAD + 16u * c);
+                    const int sel = (int)(F << 2);
+                    const u32 blo = (u32)__builtin_amdgcn_ds_bpermute(sel, (int)(u32)mb);
+                    const u32 bhi = (u32)__builtin_amdgcn_ds_bpermute(sel, (int)(u32)(mb >> 32));
+                    const u64 p = ((((u64)bhi) << 32) | (blo & ~127u)) + 128u * k + 16u * c;
+                    *reinterpret_cast<g_uint4 *>(p) = v4u_t{v.x, v.y, v.z, v.w};
+                }
+                return;
+            }
+        }
 #pragma unroll
         for (u32 j = 0; j < 8; j++) {
             const u32 F = 8u * j + r;

@@ -789,7 +789,10 @@ def main():
             "vs_baseline": None,
             "dtype": "u32",
             "data": "synthetic (SplitMix64 payload on device, RFC test keys)",
-            "config": {"workload": names[args.config], "frames_per_gpu": wl.count,
+            "config": {"workload": names[args.config] + (
+                           f", input offsets {args.in_align}-byte / output offsets {args.out_align}-byte aligned"
+                           if args.config.startswith("zipf") else ""),
+                       "frames_per_gpu": wl.count,
                        "payload_bytes_per_gpu": wl.payload_bytes, "parallelism": f"shard{world}",
                        "frames_per_s": round(wl.count * world * args.steps / elapsed, 1)},
             # bound: the roof that binds is VALU issue; achieved / peak / frac are the

@@ -46,7 +46,7 @@ public:
         }
         for (DevBuf *b : {&keys_, &desc_, &in_, &out_, &status_, &nonces_})
             b->release();
-        for (HostBuf *b : {&hdesc_, &hstatus_, &hnonces_})
+        for (HostBuf *b : {&hdesc_, &hstatus_, &hnonces_, &hin_, &hout_})
             b->release();
     }
 
@@ -115,24 +115,25 @@ public:
         hipError_t e;
         (void)hipSetDevice(device_);
         if ((e = desc_.reserve(sizeof(cz_frame_desc) * (uint64_t)count)) != hipSuccess ||
-            (e = in_.reserve(ib + 16)) != hipSuccess || (e = out_.reserve(ob + 16)) != hipSuccess)
+            (e = in_.reserve(ib + 16)) != hipSuccess || (e = out_.reserve(ob + 16)) != hipSuccess ||
+            (e = hin_.reserve(ib + 16)) != hipSuccess || (e = hout_.reserve(ob + 16)) != hipSuccess)
             return hip_fail(e, "hipMalloc");
+        // the frames gathered into pinned staging, one H2D; one D2H back, scattered on the host
+        uint8_t *hs = (uint8_t *)hin_.ptr;
         for (uint32_t i = 0; i < count; i++)
-            if (len[i] && (e = hipMemcpyAsync((uint8_t *)in_.ptr + d[i].in_off, h_in + in_off[i], len[i],
-                                              hipMemcpyHostToDevice, stream_)) != hipSuccess)
-                return hip_fail(e, "H2D");
-        if ((e = hipMemcpyAsync(desc_.ptr, d.data(), sizeof(cz_frame_desc) * (uint64_t)count, hipMemcpyHostToDevice,
+            if (len[i])
+                memcpy(hs + d[i].in_off, h_in + in_off[i], len[i]);
+        if ((e = hipMemcpyAsync(in_.ptr, hs, ib, hipMemcpyHostToDevice, stream_)) != hipSuccess ||
+            (e = hipMemcpyAsync(desc_.ptr, d.data(), sizeof(cz_frame_desc) * (uint64_t)count, hipMemcpyHostToDevice,
                                 stream_)) != hipSuccess ||
             (e = czk_seal_desc((const cz_frame_desc *)desc_.ptr, nullptr, count, in_.ptr, out_.ptr, keys_.ptr,
-                               stream_)) != hipSuccess)
+                               stream_)) != hipSuccess ||
+            (e = hipMemcpyAsync(hout_.ptr, out_.ptr, ob, hipMemcpyDeviceToHost, stream_)) != hipSuccess ||
+            (e = hipStreamSynchronize(stream_)) != hipSuccess)
             return hip_fail(e, "seal");
+        const uint8_t *ho = (const uint8_t *)hout_.ptr;
         for (uint32_t i = 0; i < count; i++)
-            if ((e = hipMemcpyAsync(h_out + out_off[i], (uint8_t *)out_.ptr + d[i].out_off,
-                                    len[i] + (uint64_t)CZ_MESSAGE_OVERHEAD, hipMemcpyDeviceToHost, stream_)) !=
-                hipSuccess)
-                return hip_fail(e, "D2H");
-        if ((e = hipStreamSynchronize(stream_)) != hipSuccess)
-            return hip_fail(e, "sync");
+            memcpy(h_out + out_off[i], ho + d[i].out_off, len[i] + (uint64_t)CZ_MESSAGE_OVERHEAD);
         cn_nonce_ += count;
         return CZ_OK;
     }
@@ -186,13 +187,15 @@ public:
         if ((e = desc_.reserve(sizeof(cz_frame_desc) * (uint64_t)count)) != hipSuccess ||
             (e = in_.reserve(ib + 16)) != hipSuccess || (e = out_.reserve(ob + 16)) != hipSuccess ||
             (e = status_.reserve(2ull * count)) != hipSuccess || (e = nonces_.reserve(8ull * count)) != hipSuccess ||
-            (e = hstatus_.reserve(2ull * count)) != hipSuccess || (e = hnonces_.reserve(8ull * count)) != hipSuccess)
+            (e = hstatus_.reserve(2ull * count)) != hipSuccess || (e = hnonces_.reserve(8ull * count)) != hipSuccess ||
+            (e = hin_.reserve(ib + 16)) != hipSuccess || (e = hout_.reserve(ob + 16)) != hipSuccess)
             return hip_fail(e, "alloc");
+        uint8_t *hs = (uint8_t *)hin_.ptr;
         for (uint32_t i = 0; i < count; i++)
-            if (size[i] && (e = hipMemcpyAsync((uint8_t *)in_.ptr + d[i].in_off, h_in + in_off[i], size[i],
-                                               hipMemcpyHostToDevice, stream_)) != hipSuccess)
-                return hip_fail(e, "H2D");
-        if ((e = hipMemcpyAsync(desc_.ptr, d.data(), sizeof(cz_frame_desc) * (uint64_t)count, hipMemcpyHostToDevice,
+            if (size[i])
+                memcpy(hs + d[i].in_off, h_in + in_off[i], size[i]);
+        if ((e = hipMemcpyAsync(in_.ptr, hs, ib, hipMemcpyHostToDevice, stream_)) != hipSuccess ||
+            (e = hipMemcpyAsync(desc_.ptr, d.data(), sizeof(cz_frame_desc) * (uint64_t)count, hipMemcpyHostToDevice,
                                 stream_)) != hipSuccess ||
             (e = czk_open_desc((const cz_frame_desc *)desc_.ptr, nullptr, count, in_.ptr, out_.ptr, keys_.ptr,
                                (uint16_t *)status_.ptr, (uint64_t *)nonces_.ptr, stream_)) != hipSuccess ||
@@ -209,11 +212,16 @@ public:
         for (; ok < count; ok++)
             if ((st[ok] & 0xff) != CZ_STATUS_OK)
                 break;
+        // the accepted frames' plaintext: one D2H of their slots, scattered on the host
+        const uint64_t okb = ok ? d[ok - 1].out_off + ((size[ok - 1] - CZ_MESSAGE_OVERHEAD + 15ull) & ~15ull) : 0;
+        if (okb && ((e = hipMemcpyAsync(hout_.ptr, out_.ptr, okb, hipMemcpyDeviceToHost, stream_)) != hipSuccess ||
+                    (e = hipStreamSynchronize(stream_)) != hipSuccess))
+            return hip_fail(e, "D2H");
+        const uint8_t *ho = (const uint8_t *)hout_.ptr;
         for (uint32_t i = 0; i < ok; i++) {
             uint64_t plen = size[i] - CZ_MESSAGE_OVERHEAD;
-            if (plen && (e = hipMemcpyAsync(h_out + out_off[i], (uint8_t *)out_.ptr + d[i].out_off, plen,
-                                            hipMemcpyDeviceToHost, stream_)) != hipSuccess)
-                return hip_fail(e, "D2H");
+            if (plen)
+                memcpy(h_out + out_off[i], ho + d[i].out_off, plen);
             if (msg_flags)  // only MORE and COMMAND reach the Msg (CurveClientMechanism.java:207-213)
                 msg_flags[i] = (uint8_t)(((st[i] >> 8) & 0x01 ? CZ_MSG_MORE : 0) | ((st[i] >> 8) & 0x02 ? CZ_MSG_COMMAND : 0));
         }
@@ -252,6 +260,7 @@ private:
     hipStream_t stream_ = nullptr;
     DevBuf keys_, desc_, in_, out_, status_, nonces_;
     HostBuf hdesc_, hstatus_, hnonces_;
+    HostBuf hin_, hout_;  // pinned staging: one H2D and one D2H per batch, not one per frame
 };
 
 }  // namespace jeromq_amd

@@ -11,21 +11,27 @@ rc=$?; tail -2 gpurun_out/pytest_gpu.log; [ $rc -eq 0 ] || exit $rc
 echo "== smoke"
 timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke()" > gpurun_out/smoke.log 2>&1 || { tail gpurun_out/smoke.log; exit 3; }
 tail -1 gpurun_out/smoke.log
-for cfg in 4k 100b zipf open4k zipf_lane; do
-  echo "== bench $cfg"
-  extra=""; [ $cfg = 4k ] || extra="--no-cpu-baseline"
-  timeout -k 10 300 python bench.py --config $cfg $extra > gpurun_out/bench_$cfg.log 2>&1 || { tail gpurun_out/bench_$cfg.log; exit 4; }
-  tail -1 gpurun_out/bench_$cfg.log | cut -c1-400
+run() {  # name, bench args
+  local name=$1; shift
+  echo "== bench $name"
+  timeout -k 10 300 python bench.py "$@" > gpurun_out/bench_$name.log 2>&1 || { tail gpurun_out/bench_$name.log; exit 4; }
+  tail -1 gpurun_out/bench_$name.log | cut -c1-400
+}
+run 4k --config 4k
+run 4k_dense --config 4k_dense --no-cpu-baseline
+run 100b --config 100b --no-cpu-baseline
+run zipf --config zipf --no-cpu-baseline
+run zipf_oa8 --config zipf --in-align 8 --out-align 8 --no-cpu-baseline
+run zipf_oa1 --config zipf --out-align 1 --no-cpu-baseline
+run open4k --config open4k --no-cpu-baseline
+run zipf_lane --config zipf_lane --no-cpu-baseline
+for cfg in e2e4k engine beforenm nacl; do
+  run $cfg --steps 10 --warmup 2 --config $cfg --no-cpu-baseline
 done
-for cfg in e2e4k engine beforenm; do
-  echo "== bench $cfg"
-  timeout -k 10 300 python bench.py --steps 10 --warmup 2 --config $cfg --no-cpu-baseline > gpurun_out/bench_$cfg.log 2>&1 || { tail gpurun_out/bench_$cfg.log; exit 5; }
-  tail -1 gpurun_out/bench_$cfg.log | cut -c1-300
-done
-for cfg in 4k zipf open4k 100b; do
+for cfg in 4k zipf open4k 100b 4k_dense; do
   echo "== rocprofv3 kernel trace $cfg"
   timeout -k 10 300 rocprofv3 --kernel-trace --stats -T --output-format csv -d gpurun_out/prof_$cfg -o run -- python3 bench.py --steps 10 --warmup 2 --no-cpu-baseline --no-roundtrip --config $cfg > gpurun_out/prof_$cfg.log 2>&1 || { tail gpurun_out/prof_$cfg.log; exit 6; }
 done
-bash tools/gpu_traffic.sh 4k 100b zipf open4k || exit 7
-bash tools/gpu_valu.sh 4k 100b zipf open4k || exit 8
+bash tools/gpu_traffic.sh 4k 100b zipf open4k 4k_dense || exit 7
+bash tools/gpu_valu.sh 4k 100b zipf open4k 4k_dense || exit 8
 exit 0

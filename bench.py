@@ -44,7 +44,7 @@ def parse():
     ap.add_argument("--ramp-ms", type=float, default=150.0,
                     help="untimed launches before the W warmup steps until this much GPU time has passed: "
                          "the clock needs ~100 ms of load to leave its idle state")
-    ap.add_argument("--seg-blocks", type=int, default=64, help="zipf: segment length in 64-byte blocks")
+    ap.add_argument("--seg-blocks", type=int, default=128, help="zipf: segment length in 64-byte blocks")
     ap.add_argument("--in-align", type=int, default=64,
                     help="zipf: input payload slot alignment in bytes (lengths are 64-byte multiples)")
     ap.add_argument("--out-align", type=int, default=128,
@@ -122,7 +122,7 @@ def shard_plan(rank, frames_per_rank, cfg="4k"):
 class Workload:
     """Builds one rank's device-resident batch and the per-step launch."""
 
-    def __init__(self, cfg, frames, rank, dev, out_align=128, seg_blocks=64, in_align=64):
+    def __init__(self, cfg, frames, rank, dev, out_align=128, seg_blocks=128, in_align=64):
         self.cfg = cfg
         self.dev = dev
         key = torch.tensor(list(PRECOM), dtype=torch.uint8, device=dev).view(1, 32)

@@ -120,7 +120,7 @@ DESC_DTYPE = np.dtype([("in_off", "<u8"), ("out_off", "<u8"), ("len", "<u4"), ("
 
 SEGMENT_DTYPE = np.dtype([("frame", "<u4"), ("first_block", "<u4"), ("nblocks", "<u4"), ("part", "<u4")])
 COMBINE_DTYPE = np.dtype([("frame", "<u4"), ("part0", "<u4"), ("nseg", "<u4"), ("reserved", "<u4")])
-SEG_BLOCKS = 64  # 4 KiB of box per lane: balances Zipf batches whose frames reach 64 KiB
+SEG_BLOCKS = 128  # 8 KiB of box per lane (Zipf sweep: 64 -> 1664, 128 -> 1687-1709, 160 -> 1707, 192 -> 1671 GiB/s)
 
 
 class SegmentPlan:

@@ -35,7 +35,7 @@ using namespace czi;
 namespace {
 
 constexpr uint64_t SLOT_ALIGN = 128;  // body / payload slots: line-staged stores, whole-line loads
-constexpr uint32_t SEG_BLOCKS = 64;
+constexpr uint32_t SEG_BLOCKS = 128;  // as jeromq_amd.batch.SEG_BLOCKS
 
 uint64_t round_up(uint64_t v, uint64_t a) { return (v + a - 1) / a * a; }
 

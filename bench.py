@@ -604,6 +604,24 @@ def load_pmc(cfg):
 VALU_PEAK_G = 256 * 4 * 2.4 / 4
 
 
+def hbm_copy_ceiling(dev, nbytes=1 << 31, reps=10):
+    """Device-to-device copy of nbytes (torch copy_, HIP events): (read + write bytes) / time, GB/s."""
+    src = torch.empty(nbytes, dtype=torch.uint8, device=dev)
+    dst = torch.empty_like(src)
+    for _ in range(2):
+        dst.copy_(src)
+    s = torch.cuda.current_stream()
+    a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    a.record(s)
+    for _ in range(reps):
+        dst.copy_(src)
+    b.record(s)
+    torch.cuda.synchronize()
+    gbs = 2 * nbytes * reps / (a.elapsed_time(b) / 1e3) / 1e9
+    del src, dst
+    return round(gbs, 1)
+
+
 def valu_roofline(pmc, kernel_s):
     n = pmc.get("valu_insts_per_launch")
     if not n:
@@ -753,6 +771,7 @@ def main():
     value = total_payload / elapsed / 2**30
     alg_bytes = wl.read_bytes + wl.write_bytes
     achieved = alg_bytes / avg_kernel_s / 1e9
+    copy_gbs = hbm_copy_ceiling(dev) if rank == 0 else None
     pmc = load_pmc(args.config)
     traffic = pmc.get("hbm_bytes_per_launch")
 
@@ -801,6 +820,10 @@ def main():
                          "frac": round(achieved / HBM_PEAK_GBS, 4),
                          "traffic": traffic,
                          "kernel_ms": round(avg_kernel_s * 1e3, 4),
+                         # the same bytes against the device-to-device copy rate
+                         # measured on this GPU in this process (read + write bytes / time)
+                         "hbm_copy_GBps": copy_gbs,  # torch copy_ of 2 GiB, HIP events, 10 reps
+                         "frac_of_copy": round(achieved / copy_gbs, 4) if copy_gbs else None,
                          "alg_bytes_per_launch": alg_bytes,
                          "valu": valu_roofline(pmc, avg_kernel_s)},
             "cpu_baseline": cpu,

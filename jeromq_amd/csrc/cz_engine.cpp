@@ -436,7 +436,9 @@ struct cz_engine {
         // every group issued before any parsing so the copies run while the host parses and plans;
         // `stream`: metadata H2D; ps[1]: unpack + open; ps[2]: D2H.  (A gather kernel reading the
         // receive buffers over PCIe instead of the per-connection DMAs measured slower, and so did
-        // spreading the DMAs over two streams: 23 against 27 GiB/s.)
+        // spreading the DMAs over two streams, 23 against 27 GiB/s, and gathering each group into
+        // one pinned slab on 8 host threads for one DMA per group, 25 GiB/s: the memcpy is slower
+        // than the gaps it removes.)
         hipStream_t qh = ps[0], qk = ps[1], qo = ps[2], qm = stream;
         std::vector<hipEvent_t> ev(groups.size(), nullptr);
         EvGuard evguard{ev};

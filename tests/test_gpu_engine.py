@@ -273,3 +273,57 @@ def test_engine_pipelined_flush_out_and_iov(torch_dev, L):
     cli.flush_out()
     assert cli.wire_out(cc[1]) == v2_encode(or_curve_encode(b"after", 0, 3 + 24, 0, _precom(1)))
     assert cli.wire_out(cc[2]) == b"" and cli.wire_iov(cc[2]) == []
+
+
+@pytest.mark.parametrize("seed", range(3))
+def test_engine_fuzz_roundtrip(torch_dev, L, seed):
+    """Randomized engine traffic: 1..10 connections, edge-biased sizes up to 1 MiB, sends
+    interleaved at random, several flush_out calls; every connection's wire stream equals the
+    V2-framed oracle seal of its messages, and the server engine, fed the streams in random
+    pieces across flush_in calls (tens of MiB, so both flushes run as several pipelined groups),
+    delivers exactly what was sent with the reference's nonce bookkeeping."""
+    from jeromq_amd.engine import CurveBatchEngine
+    rng = np.random.default_rng(500 + seed)
+    ncon = int(rng.integers(1, 11))
+    cli = CurveBatchEngine(arena_bytes=192 << 20)
+    srv = CurveBatchEngine(arena_bytes=1 << 20)
+    cc = [cli.add_connection(_precom(i)) for i in range(ncon)]
+    sc = [srv.add_connection(_precom(i), as_server=True) for i in range(ncon)]
+    edges = [0, 1, 30, 31, 32, 222, 223, 255, 256, 4096, 65536, 300000]
+    sent = {i: [] for i in range(ncon)}
+    wires = {i: bytearray() for i in range(ncon)}
+    nonce = {i: 3 for i in range(ncon)}
+    for _flush in range(int(rng.integers(1, 4))):
+        queued = {i: [] for i in range(ncon)}
+        for _ in range(int(rng.integers(20, 160))):
+            i = int(rng.integers(0, ncon))
+            r = rng.random()
+            n = (int(rng.choice(edges)) if r < 0.45 else int(rng.integers(0, 20000)) if r < 0.85
+                 else int(rng.integers(256 << 10, 1 << 20)))
+            msg = (splitmix_bytes(n, int(rng.integers(0, 1 << 30))), int(rng.integers(0, 4)))
+            assert cli.send(cc[i], msg[0], more=bool(msg[1] & 1), command=bool(msg[1] & 2)) == 0
+            queued[i].append(msg)
+        cli.flush_out()
+        for i in range(ncon):
+            w = cli.wire_out(cc[i])
+            assert w == _oracle_wire(queued[i], _precom(i), 0, nonce[i]), f"connection {i}"
+            assert b"".join(ctypes.string_at(a, n) for a, n in cli.wire_iov(cc[i])) == w
+            nonce[i] += len(queued[i])
+            sent[i] += queued[i]
+            wires[i] += w
+    got = {i: [] for i in range(ncon)}
+    pos = {i: 0 for i in range(ncon)}
+    while any(pos[i] < len(wires[i]) for i in range(ncon)):
+        for i in range(ncon):
+            if pos[i] < len(wires[i]) and rng.random() < 0.8:
+                step = int(rng.integers(1, 3 << 20))
+                srv.recv(sc[i], bytes(wires[i][pos[i]:pos[i] + step]))
+                pos[i] += step
+        srv.flush_in()
+        for i in range(ncon):
+            got[i] += srv.messages_in(sc[i])
+    for i in range(ncon):
+        assert srv.error(sc[i]) == (0, 0)
+        assert got[i] == sent[i], f"connection {i}"
+        if sent[i]:
+            assert srv.peer_nonce(sc[i]) == 3 + len(sent[i]) - 1

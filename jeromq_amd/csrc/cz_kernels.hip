@@ -214,13 +214,7 @@ __device__ __forceinline__ void st16(uint8_t *__restrict__ p, u32 a, u32 b, u32 
 // Store the first nb (0..16) bytes of a 16-byte chunk.
 __device__ __forceinline__ void st_bytes(uint8_t *__restrict__ p, u32 a, u32 b, u32 c, u32 d, u32 nb)
 {
-#ifdef CZ_XP_BYTE_LOOP
-    u32 w[4] = {a, b, c, d};
-    for (u32 i = 0; i < nb; i++)
-        p[i] = (uint8_t)(w[i >> 2] >> (8 * (i & 3)));
-#else
     st_range16(p, make_uint4(a, b, c, d), 0u, nb);
-#endif
 }
 
 __device__ __forceinline__ u32 funnel(u32 hi, u32 lo, u32 sh) { return __builtin_amdgcn_alignbyte(hi, lo, sh); }
@@ -1839,11 +1833,7 @@ __global__ __launch_bounds__(BLOCK) CZ_OCC void k_seal_uniform(const uint8_t *__
     uint32_t i = blockIdx.x * BLOCK + threadIdx.x;
     if constexpr (ST == ST_SHIFT) {
         // waves of one line phase (EmitShiftLines): a full workgroup's frames sorted by class
-#ifndef CZ_XP_NO_PERMUTE
         if (blockIdx.x * BLOCK + BLOCK <= count)
-#else
-        if (false)
-#endif
             i = blockIdx.x * BLOCK + class_permute(((uintptr_t)(out + (uint64_t)i * out_stride) & 64u) != 0);
     }
     const uint32_t wave_first = (blockIdx.x * BLOCK + threadIdx.x) & ~63u;

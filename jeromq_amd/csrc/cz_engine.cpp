@@ -39,24 +39,6 @@ constexpr uint32_t SEG_BLOCKS = 128;  // as jeromq_amd.batch.SEG_BLOCKS (DESIGN.
 
 uint64_t round_up(uint64_t v, uint64_t a) { return (v + a - 1) / a * a; }
 
-// grow a pinned buffer to hold `want` bytes, keeping its first `used` bytes
-hipError_t grow_keep(HostBuf &b, uint64_t used, uint64_t want)
-{
-    if (want <= b.cap)
-        return hipSuccess;
-    void *p = nullptr;
-    const uint64_t cap = std::max<uint64_t>({want, 2 * b.cap, 65536});
-    hipError_t e = hipHostMalloc(&p, cap, hipHostMallocDefault);
-    if (e != hipSuccess)
-        return e;
-    if (used)
-        memcpy(p, b.ptr, used);
-    b.release();
-    b.ptr = p;
-    b.cap = cap;
-    return hipSuccess;
-}
-
 // CZ_ENGINE_TRACE=1: per-phase wall times of each flush on stderr (profiling aid)
 struct PhaseTimer {
     bool on;
@@ -89,6 +71,78 @@ struct Run {
     uint64_t off, len;
 };
 
+// A connection's receive buffer: a region of one of the engine's pinned receive blocks.
+struct RxBuf {
+    uint8_t *ptr = nullptr;
+    uint64_t cap = 0;
+    uint32_t blk = 0;
+};
+
+// Pinned receive blocks shared by every connection.  Regions are bump-allocated, so connections
+// that receive together lie next to each other and flush_in moves a run of them with one DMA
+// (each DMA costs a ~25 us gap on the SDMA queue, about the time of a 1 MiB copy).  A region that
+// grows extends in place when it is the last one of its block; otherwise it moves and its old
+// space goes to a first-fit free list.
+struct RxPool {
+    struct Block {
+        uint8_t *base;
+        uint64_t cap, used;
+    };
+    std::vector<Block> blocks;
+    std::vector<RxBuf> free_list;
+    uint64_t total = 0;
+
+    ~RxPool()
+    {
+        for (Block &b : blocks)
+            (void)hipHostFree(b.base);
+    }
+    // grow r to hold `want` bytes, keeping its first `used` bytes
+    hipError_t grow(RxBuf &r, uint64_t used, uint64_t want)
+    {
+        if (want <= r.cap)
+            return hipSuccess;
+        const uint64_t cap = (std::max<uint64_t>({want, 2 * r.cap, 65536}) + 255) & ~255ull;
+        if (r.ptr) {
+            Block &b = blocks[r.blk];
+            if (r.ptr + r.cap == b.base + b.used && b.used - r.cap + cap <= b.cap) {
+                b.used += cap - r.cap;
+                r.cap = cap;
+                return hipSuccess;
+            }
+        }
+        RxBuf n;
+        size_t fi = 0;
+        for (; fi < free_list.size() && free_list[fi].cap < cap; fi++) {
+        }
+        if (fi < free_list.size()) {
+            n = free_list[fi];
+            free_list.erase(free_list.begin() + (long)fi);
+        } else {
+            if (blocks.empty() || blocks.back().cap - blocks.back().used < cap) {
+                // blocks grow with the pool: 1 MiB .. 256 MiB, or one region's size
+                const uint64_t bcap = std::max<uint64_t>(cap, std::min<uint64_t>(256ull << 20,
+                                                                                std::max<uint64_t>(1ull << 20, total)));
+                void *p = nullptr;
+                hipError_t e = hipHostMalloc(&p, bcap, hipHostMallocDefault);
+                if (e != hipSuccess)
+                    return e;
+                blocks.push_back({(uint8_t *)p, bcap, 0});
+                total += bcap;
+            }
+            Block &b = blocks.back();
+            n = {b.base + b.used, cap, (uint32_t)(blocks.size() - 1)};
+            b.used += cap;
+        }
+        if (used)
+            memcpy(n.ptr, r.ptr, used);
+        if (r.ptr)
+            free_list.push_back(r);
+        r = n;
+        return hipSuccess;
+    }
+};
+
 struct Conn {
     bool server = false;
     uint32_t tx_key = 0, rx_key = 0;  // subkey table indices
@@ -96,7 +150,7 @@ struct Conn {
     uint64_t peer_nonce = 0;          // cnPeerNonce: last accepted peer nonce
     int error = 0;                    // CZ_EPROTO / CZ_EMSGSIZE once torn down
     int event = 0;                    // ZMTP protocol-error event of the failure
-    HostBuf rx;                       // received bytes not yet parsed, pinned (DMA'd as they lie)
+    RxBuf rx;                         // received bytes not yet parsed, pinned (DMA'd as they lie)
     uint64_t rx_len = 0;
     std::vector<Run> runs;            // wire stream of the last flush_out: pieces of h_wire, in send order
     std::vector<uint8_t> gathered;    // contiguous copy for cz_engine_wire_out when runs > 1
@@ -159,6 +213,7 @@ struct cz_engine {
     DevBuf d_in, d_body, d_wire, d_desc, d_seg, d_comb, d_work, d_items, d_status, d_nonces, d_plain;
     HostBuf h_status, h_nonces;
     HostBuf h_meta;  // pinned staging of descriptors / items / segment lists (async H2D)
+    RxPool rxpool;   // every connection's receive buffer
 
     ~cz_engine()
     {
@@ -177,8 +232,6 @@ struct cz_engine {
             b->release();
         for (HostBuf *b : {&arena, &h_wire, &h_plain, &h_status, &h_nonces, &h_meta})
             b->release();
-        for (Conn &c : conns)
-            c.rx.release();
     }
 
     Conn *conn(int c)
@@ -432,35 +485,65 @@ struct cz_engine {
             if ((e = hipEventCreateWithFlags(&evm[gi], hipEventDisableTiming)) != hipSuccess ||
                 (e = hipEventCreateWithFlags(&evk[gi], hipEventDisableTiming)) != hipSuccess)
                 return hip_fail(e, "hipEventCreate");
-        // ps[0]: received bytes H2D, one DMA per connection straight from its pinned receive buffer,
-        // every group issued before any parsing so the copies run while the host parses and plans;
-        // `stream`: metadata H2D; ps[1]: unpack + open; ps[2]: D2H.  (A gather kernel reading the
-        // receive buffers over PCIe instead of the per-connection DMAs measured slower, and so did
-        // spreading the DMAs over two streams, 23 against 27 GiB/s, and gathering each group into
-        // one pinned slab on 8 host threads for one DMA per group, 25 GiB/s: the memcpy is slower
-        // than the gaps it removes.)
+        // ps[0]: received bytes H2D straight from the pinned receive blocks, one DMA per run of
+        // connections that lie next to each other there (RxPool), every group issued before any
+        // parsing so the copies run while the host parses and plans; `stream`: metadata H2D;
+        // ps[1]: unpack + open; ps[2]: D2H.  (A gather kernel reading the receive buffers over PCIe
+        // instead of DMAs measured slower, and so did spreading the DMAs over two streams, gathering
+        // each group into one pinned slab on 8 host threads (the memcpy is slower than the gaps it
+        // removes) and hipMemcpyBatchAsync of the per-connection copies (the same gaps).)
         hipStream_t qh = ps[0], qk = ps[1], qo = ps[2], qm = stream;
         std::vector<hipEvent_t> ev(groups.size(), nullptr);
         EvGuard evguard{ev};
         for (size_t gi = 0; gi < groups.size(); gi++)
             if ((e = hipEventCreateWithFlags(&ev[gi], hipEventDisableTiming)) != hipSuccess)
                 return hip_fail(e, "hipEventCreate");
+        // spans: a group's connections in address order, merged while they share a receive block
+        // and the bytes between them (other connections' spare capacity) are at most MERGE_GAP --
+        // copying those costs less than another DMA's gap
+        struct Span {
+            const uint8_t *src;
+            uint64_t dev, len;
+        };
+        std::vector<Span> spans;
+        std::vector<size_t> span_end(groups.size());
         {
+            constexpr uint64_t MERGE_GAP = 1ull << 20;
             uint64_t off = 0;
-            for (Parsed &p : parsed) {
-                p.rx_off = off;
-                off += conns[p.conn].rx_len;
+            std::vector<size_t> order;
+            for (size_t gi = 0; gi < groups.size(); gi++) {
+                order.clear();
+                for (size_t pi = groups[gi].pa; pi < groups[gi].pb; pi++)
+                    order.push_back(pi);
+                std::sort(order.begin(), order.end(),
+                          [&](size_t x, size_t y) { return conns[parsed[x].conn].rx.ptr < conns[parsed[y].conn].rx.ptr; });
+                uint32_t blk = 0;
+                for (size_t pi : order) {
+                    Parsed &p = parsed[pi];
+                    const Conn &c = conns[p.conn];
+                    Span *last = spans.size() > (gi ? span_end[gi - 1] : 0) ? &spans.back() : nullptr;
+                    if (last && c.rx.blk == blk && c.rx.ptr <= last->src + last->len + MERGE_GAP) {
+                        p.rx_off = last->dev + (uint64_t)(c.rx.ptr - last->src);
+                        const uint64_t end = (uint64_t)(c.rx.ptr + c.rx_len - last->src);
+                        off += end - last->len;
+                        last->len = end;
+                    } else {
+                        p.rx_off = off;
+                        spans.push_back({c.rx.ptr, off, c.rx_len});
+                        off += c.rx_len;
+                        blk = c.rx.blk;
+                    }
+                }
+                span_end[gi] = spans.size();
             }
             if (off && (e = d_wire.reserve(off)) != hipSuccess)
                 return hip_fail(e, "cz_engine: alloc");
         }
-        for (size_t gi = 0; gi < groups.size(); gi++) {
-            for (size_t pi = groups[gi].pa; pi < groups[gi].pb; pi++) {
-                const Parsed &p = parsed[pi];
-                if ((e = hipMemcpyAsync((uint8_t *)d_wire.ptr + p.rx_off, conns[p.conn].rx.ptr, conns[p.conn].rx_len,
+        for (size_t gi = 0, si = 0; gi < groups.size(); gi++) {
+            for (; si < span_end[gi]; si++)
+                if ((e = hipMemcpyAsync((uint8_t *)d_wire.ptr + spans[si].dev, spans[si].src, spans[si].len,
                                         hipMemcpyHostToDevice, qh)) != hipSuccess)
                     return hip_fail(e, "cz_engine: H2D");
-            }
             if ((e = hipEventRecord(ev[gi], qh)) != hipSuccess)
                 return hip_fail(e, "cz_engine: H2D");
         }
@@ -870,7 +953,7 @@ int cz_engine_recv(cz_engine *e, int conn, const void *wire, uint64_t len)
         return CZ_EINVAL;
     if (c->error)
         return fail(c->error, "cz_engine_recv: connection %d has failed", conn);
-    hipError_t he = grow_keep(c->rx, c->rx_len, c->rx_len + len);
+    hipError_t he = e->rxpool.grow(c->rx, c->rx_len, c->rx_len + len);
     if (he != hipSuccess)
         return hip_fail(he, "cz_engine_recv: hipHostMalloc");
     if (len)
@@ -888,7 +971,7 @@ int cz_engine_recv_buffer(cz_engine *e, int conn, uint64_t min_bytes, uint8_t **
         return CZ_EINVAL;
     if (c->error)
         return fail(c->error, "cz_engine_recv_buffer: connection %d has failed", conn);
-    hipError_t he = grow_keep(c->rx, c->rx_len, c->rx_len + std::max<uint64_t>(min_bytes, 1));
+    hipError_t he = e->rxpool.grow(c->rx, c->rx_len, c->rx_len + std::max<uint64_t>(min_bytes, 1));
     if (he != hipSuccess)
         return hip_fail(he, "cz_engine_recv_buffer: hipHostMalloc");
     *buf = (uint8_t *)c->rx.ptr + c->rx_len;

@@ -549,18 +549,18 @@ struct cz_engine {
         }
         pt.mark("h2d-issue");
         // 1. per group, on its own host thread: parse each connection's whole frames (V2Decoder; a
-        //    partial frame waits for more bytes), build the group's descriptors -- bodies unpacked
-        //    into aligned slots, each connection's frames chained by prev (group-relative
-        //    indices) -- and plan its segments.  Offsets are group-relative until step 2.
+        //    partial frame waits for more bytes) and count the group's frames, body / plaintext slot
+        //    bytes and segments (plan_counts) -- enough to place every group's arrays.
         struct GroupWork {
             std::vector<cz_v2_frame> frames;
-            std::vector<cz_frame_desc> desc;
-            std::vector<cz_v2_item> items;
             Segs sg;
-            uint64_t bslot = 0, pslot = 0;
+            uint64_t bslot = 0, pslot = 0;   // slot bytes of the group
+            uint64_t nseg = 0, ncomb = 0, npart = 0;
+            uint64_t b0 = 0, soff = 0, coff = 0, woff = 0;  // where its arrays start
+            bool bad_plan = false;
         };
         std::vector<GroupWork> gw(groups.size());
-        auto work = [&](size_t gi) {
+        auto parse = [&](size_t gi) {
             GroupWork &w = gw[gi];
             const Group &g = groups[gi];
             constexpr uint32_t CH = 4096;  // parse in chunks of CH frames
@@ -589,147 +589,163 @@ struct cz_engine {
                 p.consumed = consumed;
                 p.perr = prc == CZ_OK ? 0 : prc;
             }
-            const size_t gn = w.frames.size();
-            w.desc.resize(gn);
-            w.items.resize(gn);
-            for (size_t q = g.pa; q < g.pb; q++) {
-                const Parsed &p = parsed[q];
-                const Conn &c = conns[p.conn];
-                for (uint32_t k = 0; k < p.count; k++) {
-                    const uint32_t i = p.first + k;
-                    const cz_v2_frame &f = w.frames[i];
-                    const uint64_t plen = f.size > CZ_MESSAGE_OVERHEAD ? f.size - CZ_MESSAGE_OVERHEAD : 0;
-                    w.items[i] = {p.rx_off + f.body_off, w.bslot, f.size, 0u};
-                    w.desc[i] = {w.bslot, w.pslot, f.size, c.rx_key, c.peer_nonce, CZ_DESC_CHECK_NONCE,
-                                 k ? (int32_t)(i - 1) : -1};
-                    w.bslot += round_up(std::max<uint64_t>(f.size, 1), SLOT_ALIGN);
-                    w.pslot += round_up(std::max<uint64_t>(plen, 1), SLOT_ALIGN);
-                }
+            for (const cz_v2_frame &f : w.frames) {
+                const uint64_t plen = f.size > CZ_MESSAGE_OVERHEAD ? f.size - CZ_MESSAGE_OVERHEAD : 0;
+                w.bslot += round_up(std::max<uint64_t>(f.size, 1), SLOT_ALIGN);
+                w.pslot += round_up(std::max<uint64_t>(plen, 1), SLOT_ALIGN);
+                plan_counts(f.size, 1, SEG_BLOCKS, w.nseg, w.ncomb, w.npart);
             }
-            // the planner reads only lengths for open (no line phase), so relative offsets do
-            plan_segments(w.desc.data(), (uint32_t)gn, 1, SEG_BLOCKS, w.sg.seg, w.sg.comb, w.sg.npart);
-            w.sg.nseg = (uint32_t)w.sg.seg.size();
-            w.sg.ncomb = (uint32_t)w.sg.comb.size();
         };
         {
             std::vector<std::thread> th;
             for (size_t gi = 1; gi < groups.size(); gi++)
-                th.emplace_back(work, gi);
+                th.emplace_back(parse, gi);
             if (!groups.empty())
-                work(0);
+                parse(0);
             for (std::thread &t : th)
                 t.join();
         }
-        pt.mark("parse+desc+plan");
-        // 2. concatenate the groups: absolute frame indices and slot offsets
+        pt.mark("parse");
+        // 2. place the groups: absolute frame indices, slot offsets, segment-list offsets; size
+        //    every buffer once
         uint32_t n = 0;
-        uint64_t bslot = 0, pslot = 0;
+        uint64_t bslot = 0, pslot = 0, nseg = 0, ncomb = 0, npart = 0;
         for (size_t gi = 0; gi < groups.size(); gi++) {
             Group &g = groups[gi];
+            GroupWork &w = gw[gi];
             g.fa = n;
             for (size_t q = g.pa; q < g.pb; q++)
                 parsed[q].first += n;
-            n += (uint32_t)gw[gi].frames.size();
+            n += (uint32_t)w.frames.size();
             g.fb = n;
             g.pl0 = pslot;
-            for (cz_frame_desc &d : gw[gi].desc) {
-                d.in_off += bslot;
-                d.out_off += pslot;
-            }
-            for (cz_v2_item &it : gw[gi].items)
-                it.dst_off += bslot;
-            bslot += gw[gi].bslot;
-            pslot += gw[gi].pslot;
+            w.b0 = bslot;
+            w.soff = nseg;
+            w.coff = ncomb;
+            w.woff = npart;
+            bslot += w.bslot;
+            pslot += w.pslot;
+            nseg += w.nseg;
+            ncomb += w.ncomb;
+            npart += w.npart;
             g.pl1 = pslot;
         }
-        std::vector<cz_frame_desc> desc;
-        desc.reserve(n);
-        for (const GroupWork &w : gw)
-            desc.insert(desc.end(), w.desc.begin(), w.desc.end());
+        const uint64_t m_items = 0, m_desc = (uint64_t)n * sizeof(cz_v2_item),
+                       m_seg = m_desc + (uint64_t)n * sizeof(cz_frame_desc),
+                       m_comb = m_seg + nseg * sizeof(cz_segment), m_end = m_comb + ncomb * sizeof(cz_combine);
+        // (a device buffer that has to grow is reallocated here, which waits for the copies in
+        //  flight; steady-state flushes reuse their buffers)
+        if (n && ((e = d_in.reserve(bslot)) != hipSuccess || (e = d_plain.reserve(pslot)) != hipSuccess ||
+                  (e = d_items.reserve((uint64_t)n * sizeof(cz_v2_item))) != hipSuccess ||
+                  (e = d_status.reserve((uint64_t)n * 2)) != hipSuccess ||
+                  (e = d_nonces.reserve((uint64_t)n * 8)) != hipSuccess ||
+                  (e = d_desc.reserve((uint64_t)n * sizeof(cz_frame_desc))) != hipSuccess ||
+                  (e = d_seg.reserve(std::max<uint64_t>(nseg, 1) * sizeof(cz_segment))) != hipSuccess ||
+                  (e = d_comb.reserve(std::max<uint64_t>(ncomb, 1) * sizeof(cz_combine))) != hipSuccess ||
+                  (e = d_work.reserve(std::max<uint64_t>(npart, 1) * 64)) != hipSuccess ||
+                  (e = h_plain.reserve(pslot)) != hipSuccess || (e = h_status.reserve((uint64_t)n * 2)) != hipSuccess ||
+                  (e = h_nonces.reserve((uint64_t)n * 8)) != hipSuccess || (e = h_meta.reserve(m_end)) != hipSuccess))
+            return hip_fail(e, "cz_engine: alloc");
+        // the host-built arrays go straight into pinned staging (pageable sources would make each
+        // H2D synchronous); descriptors stay there for the delivery step
+        uint8_t *hm = (uint8_t *)h_meta.ptr;
+        cz_v2_item *h_items = (cz_v2_item *)(hm + m_items);
+        cz_frame_desc *h_desc = (cz_frame_desc *)(hm + m_desc);
+        cz_segment *h_seg = (cz_segment *)(hm + m_seg);
+        cz_combine *h_comb = (cz_combine *)(hm + m_comb);
+        pt.mark("place");
+        // 3. per group, on its own host thread: descriptors -- bodies unpacked into aligned slots,
+        //    each connection's frames chained by prev (group-relative indices, as the kernels get
+        //    the group's descriptor array) -- and the segment plan.  This thread issues group g's
+        //    metadata H2D, kernels and D2H as soon as its worker is done, while later groups are
+        //    still being built.
+        auto build = [&](size_t gi) {
+            GroupWork &w = gw[gi];
+            const Group &g = groups[gi];
+            cz_v2_item *items = h_items + g.fa;
+            cz_frame_desc *desc = h_desc + g.fa;
+            uint64_t bs = w.b0, ps = g.pl0;
+            for (size_t q = g.pa; q < g.pb; q++) {
+                const Parsed &p = parsed[q];
+                const Conn &c = conns[p.conn];
+                for (uint32_t k = 0; k < p.count; k++) {
+                    const uint32_t i = p.first - g.fa + k;
+                    const cz_v2_frame &f = w.frames[i];
+                    const uint64_t plen = f.size > CZ_MESSAGE_OVERHEAD ? f.size - CZ_MESSAGE_OVERHEAD : 0;
+                    items[i] = {p.rx_off + f.body_off, bs, f.size, 0u};
+                    desc[i] = {bs, ps, f.size, c.rx_key, c.peer_nonce, CZ_DESC_CHECK_NONCE, k ? (int32_t)(i - 1) : -1};
+                    bs += round_up(std::max<uint64_t>(f.size, 1), SLOT_ALIGN);
+                    ps += round_up(std::max<uint64_t>(plen, 1), SLOT_ALIGN);
+                }
+            }
+            const uint32_t gn = g.fb - g.fa;
+            plan_segments(desc, gn, 1, SEG_BLOCKS, w.sg.seg, w.sg.comb, w.sg.npart);
+            w.sg.nseg = (uint32_t)w.sg.seg.size();
+            w.sg.ncomb = (uint32_t)w.sg.comb.size();
+            if (w.sg.nseg != w.nseg || w.sg.ncomb != w.ncomb || w.sg.npart != w.npart) {
+                w.bad_plan = true;
+                return;
+            }
+            memcpy(h_seg + w.soff, w.sg.seg.data(), (uint64_t)w.sg.nseg * sizeof(cz_segment));
+            memcpy(h_comb + w.coff, w.sg.comb.data(), (uint64_t)w.sg.ncomb * sizeof(cz_combine));
+        };
+        auto issue = [&](size_t gi) -> hipError_t {
+            const Group &g = groups[gi];
+            const GroupWork &w = gw[gi];
+            const uint32_t gn = g.fb - g.fa;
+            if (gn == 0)
+                return hipSuccess;
+            cz_frame_desc *dd = (cz_frame_desc *)d_desc.ptr + g.fa;
+            cz_segment *dsg = (cz_segment *)d_seg.ptr + w.soff;
+            cz_combine *dcb = (cz_combine *)d_comb.ptr + w.coff;
+            hipError_t r;
+            // (a) metadata stream: the group's descriptors / items / segment lists
+            if ((r = hipMemcpyAsync((cz_v2_item *)d_items.ptr + g.fa, h_items + g.fa, (uint64_t)gn * sizeof(cz_v2_item),
+                                    hipMemcpyHostToDevice, qm)) != hipSuccess ||
+                (r = hipMemcpyAsync(dd, h_desc + g.fa, (uint64_t)gn * sizeof(cz_frame_desc), hipMemcpyHostToDevice,
+                                    qm)) != hipSuccess ||
+                (w.sg.nseg && (r = hipMemcpyAsync(dsg, h_seg + w.soff, (uint64_t)w.sg.nseg * sizeof(cz_segment),
+                                                  hipMemcpyHostToDevice, qm)) != hipSuccess) ||
+                (w.sg.ncomb && (r = hipMemcpyAsync(dcb, h_comb + w.coff, (uint64_t)w.sg.ncomb * sizeof(cz_combine),
+                                                   hipMemcpyHostToDevice, qm)) != hipSuccess) ||
+                (r = hipEventRecord(evm[gi], qm)) != hipSuccess)
+                return r;
+            // (b) compute stream: once the group's bytes and metadata landed, unpack + open;
+            // (c) D2H stream
+            if ((r = hipStreamWaitEvent(qk, ev[gi], 0)) != hipSuccess ||
+                (r = hipStreamWaitEvent(qk, evm[gi], 0)) != hipSuccess ||
+                (r = czk_v2_copy((const cz_v2_item *)d_items.ptr + g.fa, gn, d_wire.ptr, d_in.ptr, qk)) != hipSuccess ||
+                (r = czk_open_segments(dd, dsg, w.sg.nseg, dcb, w.sg.ncomb, d_in.ptr, d_plain.ptr, subkeys.ptr,
+                                       (uint8_t *)d_work.ptr + 64 * w.woff, (uint16_t *)d_status.ptr + g.fa,
+                                       (uint64_t *)d_nonces.ptr + g.fa, qk)) != hipSuccess ||
+                (r = hipEventRecord(evk[gi], qk)) != hipSuccess || (r = hipStreamWaitEvent(qo, evk[gi], 0)) != hipSuccess ||
+                (r = hipMemcpyAsync((uint8_t *)h_plain.ptr + g.pl0, (uint8_t *)d_plain.ptr + g.pl0, g.pl1 - g.pl0,
+                                    hipMemcpyDeviceToHost, qo)) != hipSuccess ||
+                (r = hipMemcpyAsync((uint16_t *)h_status.ptr + g.fa, (uint16_t *)d_status.ptr + g.fa, (uint64_t)gn * 2,
+                                    hipMemcpyDeviceToHost, qo)) != hipSuccess ||
+                (r = hipMemcpyAsync((uint64_t *)h_nonces.ptr + g.fa, (uint64_t *)d_nonces.ptr + g.fa, (uint64_t)gn * 8,
+                                    hipMemcpyDeviceToHost, qo)) != hipSuccess)
+                return r;
+            return hipSuccess;
+        };
         if (n) {
-            // device segment / combine / work arrays hold all groups at once
-            uint64_t nseg = 0, ncomb = 0, npart = 0;
-            std::vector<uint64_t> soff(groups.size()), coff(groups.size()), woff(groups.size());
+            std::vector<std::thread> th;
+            for (size_t gi = 1; gi < groups.size(); gi++)
+                th.emplace_back(build, gi);
+            build(0);
+            e = hipSuccess;
+            bool bad = false;
             for (size_t gi = 0; gi < groups.size(); gi++) {
-                soff[gi] = nseg;
-                coff[gi] = ncomb;
-                woff[gi] = npart;
-                nseg += gw[gi].sg.nseg;
-                ncomb += gw[gi].sg.ncomb;
-                npart += gw[gi].sg.npart;
+                if (gi)
+                    th[gi - 1].join();
+                bad = bad || gw[gi].bad_plan;
+                if (!bad && e == hipSuccess)
+                    e = issue(gi);  // after a failure: join the rest, issue nothing more
             }
-            const uint64_t m_items = 0, m_desc = (uint64_t)n * sizeof(cz_v2_item),
-                           m_seg = m_desc + (uint64_t)n * sizeof(cz_frame_desc),
-                           m_comb = m_seg + nseg * sizeof(cz_segment), m_end = m_comb + ncomb * sizeof(cz_combine);
-            // (a device buffer that has to grow is reallocated here, which waits for the copies
-            //  in flight; steady-state flushes reuse their buffers)
-            if ((e = d_in.reserve(bslot)) != hipSuccess || (e = d_plain.reserve(pslot)) != hipSuccess ||
-                (e = d_items.reserve((uint64_t)n * sizeof(cz_v2_item))) != hipSuccess ||
-                (e = d_status.reserve((uint64_t)n * 2)) != hipSuccess ||
-                (e = d_nonces.reserve((uint64_t)n * 8)) != hipSuccess ||
-                (e = d_desc.reserve((uint64_t)n * sizeof(cz_frame_desc))) != hipSuccess ||
-                (e = d_seg.reserve(std::max<uint64_t>(nseg, 1) * sizeof(cz_segment))) != hipSuccess ||
-                (e = d_comb.reserve(std::max<uint64_t>(ncomb, 1) * sizeof(cz_combine))) != hipSuccess ||
-                (e = d_work.reserve(std::max<uint64_t>(npart, 1) * 64)) != hipSuccess ||
-                (e = h_plain.reserve(pslot)) != hipSuccess || (e = h_status.reserve((uint64_t)n * 2)) != hipSuccess ||
-                (e = h_nonces.reserve((uint64_t)n * 8)) != hipSuccess || (e = h_meta.reserve(m_end)) != hipSuccess)
-                return hip_fail(e, "cz_engine: alloc");
-            // pinned copies of the host-built arrays: pageable sources would make each H2D synchronous
-            uint8_t *hm = (uint8_t *)h_meta.ptr;
-            memcpy(hm + m_desc, desc.data(), (uint64_t)n * sizeof(cz_frame_desc));
-            for (size_t gi = 0; gi < groups.size(); gi++) {
-                const GroupWork &w = gw[gi];
-                memcpy(hm + m_items + groups[gi].fa * sizeof(cz_v2_item), w.items.data(),
-                       w.items.size() * sizeof(cz_v2_item));
-                memcpy(hm + m_seg + soff[gi] * sizeof(cz_segment), w.sg.seg.data(),
-                       (uint64_t)w.sg.nseg * sizeof(cz_segment));
-                memcpy(hm + m_comb + coff[gi] * sizeof(cz_combine), w.sg.comb.data(),
-                       (uint64_t)w.sg.ncomb * sizeof(cz_combine));
-            }
-            const cz_v2_item *h_items = (const cz_v2_item *)(hm + m_items);
-            const cz_frame_desc *h_desc = (const cz_frame_desc *)(hm + m_desc);
-            const cz_segment *h_seg = (const cz_segment *)(hm + m_seg);
-            const cz_combine *h_comb = (const cz_combine *)(hm + m_comb);
-            pt.mark("desc+plan");
-            for (size_t gi = 0; gi < groups.size(); gi++) {
-                const Group &g = groups[gi];
-                const uint32_t gn = g.fb - g.fa;
-                if (gn == 0)
-                    continue;
-                const Segs &sg = gw[gi].sg;
-                cz_frame_desc *dd = (cz_frame_desc *)d_desc.ptr + g.fa;
-                cz_segment *dsg = (cz_segment *)d_seg.ptr + soff[gi];
-                cz_combine *dcb = (cz_combine *)d_comb.ptr + coff[gi];
-                // (a) metadata stream: the group's descriptors / items / segment lists
-                if ((e = hipMemcpyAsync((cz_v2_item *)d_items.ptr + g.fa, h_items + g.fa,
-                                        (uint64_t)gn * sizeof(cz_v2_item), hipMemcpyHostToDevice, qm)) != hipSuccess ||
-                    (e = hipMemcpyAsync(dd, h_desc + g.fa, (uint64_t)gn * sizeof(cz_frame_desc),
-                                        hipMemcpyHostToDevice, qm)) != hipSuccess ||
-                    (sg.nseg && (e = hipMemcpyAsync(dsg, h_seg + soff[gi], (uint64_t)sg.nseg * sizeof(cz_segment),
-                                                    hipMemcpyHostToDevice, qm)) != hipSuccess) ||
-                    (sg.ncomb && (e = hipMemcpyAsync(dcb, h_comb + coff[gi], (uint64_t)sg.ncomb * sizeof(cz_combine),
-                                                     hipMemcpyHostToDevice, qm)) != hipSuccess) ||
-                    (e = hipEventRecord(evm[gi], qm)) != hipSuccess)
-                    return hip_fail(e, "cz_engine: flush_in H2D");
-                // (b) compute stream: once the group's bytes and metadata landed, unpack + open;
-                // (c) D2H stream
-                if ((e = hipStreamWaitEvent(qk, ev[gi], 0)) != hipSuccess ||
-                    (e = hipStreamWaitEvent(qk, evm[gi], 0)) != hipSuccess ||
-                    (e = czk_v2_copy((const cz_v2_item *)d_items.ptr + g.fa, gn, d_wire.ptr, d_in.ptr, qk)) !=
-                        hipSuccess ||
-                    (e = czk_open_segments(dd, dsg, sg.nseg, dcb, sg.ncomb, d_in.ptr, d_plain.ptr, subkeys.ptr,
-                                           (uint8_t *)d_work.ptr + 64 * woff[gi], (uint16_t *)d_status.ptr + g.fa,
-                                           (uint64_t *)d_nonces.ptr + g.fa, qk)) != hipSuccess ||
-                    (e = hipEventRecord(evk[gi], qk)) != hipSuccess ||
-                    (e = hipStreamWaitEvent(qo, evk[gi], 0)) != hipSuccess ||
-                    (e = hipMemcpyAsync((uint8_t *)h_plain.ptr + g.pl0, (uint8_t *)d_plain.ptr + g.pl0,
-                                        g.pl1 - g.pl0, hipMemcpyDeviceToHost, qo)) != hipSuccess ||
-                    (e = hipMemcpyAsync((uint16_t *)h_status.ptr + g.fa, (uint16_t *)d_status.ptr + g.fa,
-                                        (uint64_t)gn * 2, hipMemcpyDeviceToHost, qo)) != hipSuccess ||
-                    (e = hipMemcpyAsync((uint64_t *)h_nonces.ptr + g.fa, (uint64_t *)d_nonces.ptr + g.fa,
-                                        (uint64_t)gn * 8, hipMemcpyDeviceToHost, qo)) != hipSuccess)
-                    return hip_fail(e, "cz_engine: flush_in");
-            }
+            if (bad)
+                return fail(CZ_EINVAL, "cz_engine: internal error, segment plan differs from its count");
+            if (e != hipSuccess)
+                return hip_fail(e, "cz_engine: flush_in");
         }
         for (hipStream_t q : {qh, qk, qo, qm})
             if ((e = hipStreamSynchronize(q)) != hipSuccess)
@@ -760,7 +776,7 @@ struct cz_engine {
                 if (fl & 0x02)
                     mf |= CZ_MSG_COMMAND;
                 c.in_msgs.push_back((uint32_t)in_msgs.size());
-                in_msgs.push_back({desc[i].out_off, desc[i].len - CZ_MESSAGE_OVERHEAD, mf});
+                in_msgs.push_back({h_desc[i].out_off, h_desc[i].len - CZ_MESSAGE_OVERHEAD, mf});
             }
             if (failed) {
                 c.rx_len = 0;

@@ -12,4 +12,5 @@ for round in 1 2 3; do
 done
 timeout -k 10 300 python bench.py --config engine > gpurun_out/bench_engine_rxpool.log 2>&1 || { tail gpurun_out/bench_engine_rxpool.log; exit 6; }
 tail -1 gpurun_out/bench_engine_rxpool.log | cut -c1-600
+CZ_ENGINE_TRACE=1 timeout -k 10 120 ./tools/bin/engine_cbench 2>&1 | tail -3
 exit 0

@@ -283,8 +283,7 @@ struct cz_engine {
             arena_used = 0;  // buffers allocated but never sent are released too
             return CZ_OK;
         }
-        std::vector<cz_frame_desc> desc(n);
-        std::vector<cz_v2_item> items(n);
+        // 1. send-order wire positions and each connection's runs
         std::vector<uint64_t> wpos(n + 1);
         uint64_t w = 0;
         for (uint32_t i = 0; i < n; i++) {
@@ -301,10 +300,14 @@ struct cz_engine {
         }
         wpos[n] = w;
         wire_total = w;
-        // groups of ~equal wire bytes: [fa, fb) in send order, body slots contiguous per group
+        // 2. groups of ~equal wire bytes: [fa, fb) in send order, body slots contiguous per group;
+        //    per group the arena prefix it needs, its body-slot base and its segment / combine
+        //    counts (plan_counts) -- enough to size every buffer and start the arena copy before
+        //    any descriptor exists
         struct Group {
             uint32_t fa, fb;
             uint64_t arena_hi;  // the arena prefix [0, arena_hi) holds every payload of groups <= this one
+            uint64_t slot0;     // first body slot
         };
         std::vector<Group> groups;
         {
@@ -312,30 +315,23 @@ struct cz_engine {
             uint32_t fa = 0;
             for (uint32_t i = 0; i < n; i++)
                 if (i + 1 == n || wpos[i + 1] * G >= w * (groups.size() + 1)) {
-                    groups.push_back({fa, i + 1, 0});
+                    groups.push_back({fa, i + 1, 0, 0});
                     fa = i + 1;
                 }
         }
+        std::vector<uint64_t> soff(groups.size() + 1, 0), coff(groups.size() + 1, 0), woff(groups.size() + 1, 0);
         uint64_t slot = 0, hi = 0;
-        for (Group &g : groups) {
+        for (size_t gi = 0; gi < groups.size(); gi++) {
+            Group &g = groups[gi];
+            g.slot0 = slot;
+            uint64_t ns = 0, nc = 0, np = 0;
             for (uint32_t i = g.fa; i < g.fb; i++) {
                 const OutMsg &m = pend[i];
-                Conn &c = conns[m.conn];
-                const uint64_t body = (uint64_t)m.len + CZ_MESSAGE_OVERHEAD;
-                desc[i] = {m.arena_off, slot, m.len, c.tx_key, c.nonce++, m.flags & 0xffu, -1};
-                items[i] = {slot, wpos[i], (uint32_t)body, (uint32_t)CZ_V2_ITEM_HEADER};
-                slot += round_up(body, SLOT_ALIGN);
+                slot += round_up((uint64_t)m.len + CZ_MESSAGE_OVERHEAD, SLOT_ALIGN);
                 hi = std::max<uint64_t>(hi, m.arena_off + m.len);
+                plan_counts(m.len, 0, SEG_BLOCKS, ns, nc, np);
             }
             g.arena_hi = hi;
-        }
-        // segment / combine counts per group (the plans themselves are made inside the loop, each
-        // while the copies issued before it run); the device arrays hold all groups at once
-        std::vector<uint64_t> soff(groups.size() + 1, 0), coff(groups.size() + 1, 0), woff(groups.size() + 1, 0);
-        for (size_t gi = 0; gi < groups.size(); gi++) {
-            uint64_t ns = 0, nc = 0, np = 0;
-            for (uint32_t i = groups[gi].fa; i < groups[gi].fb; i++)
-                plan_counts(desc[i].len, 0, SEG_BLOCKS, ns, nc, np);
             soff[gi + 1] = soff[gi] + ns;
             coff[gi + 1] = coff[gi] + nc;
             woff[gi + 1] = woff[gi] + np;
@@ -354,11 +350,12 @@ struct cz_engine {
             (e = d_work.reserve(std::max<uint64_t>(npart, 1) * 64)) != hipSuccess ||
             (e = h_wire.reserve(wire_total)) != hipSuccess || (e = h_meta.reserve(m_end)) != hipSuccess)
             return hip_fail(e, "cz_engine: alloc");
-        // pinned copies of the host-built arrays: pageable sources would make each H2D synchronous
+        // descriptors and items are built straight into pinned staging (pageable sources would
+        // make each H2D synchronous), one group at a time while the copies issued before run
         uint8_t *hm = (uint8_t *)h_meta.ptr;
-        memcpy(hm + m_items, items.data(), (uint64_t)n * sizeof(cz_v2_item));
-        memcpy(hm + m_desc, desc.data(), (uint64_t)n * sizeof(cz_frame_desc));
-        pt.mark("desc");
+        cz_v2_item *h_items = (cz_v2_item *)(hm + m_items);
+        cz_frame_desc *h_desc = (cz_frame_desc *)(hm + m_desc);
+        pt.mark("plan");
         std::vector<hipEvent_t> ev(groups.size(), nullptr), evk(groups.size(), nullptr);
         EvGuard evguard{ev}, evkguard{evk};
         for (size_t gi = 0; gi < groups.size(); gi++)
@@ -382,21 +379,30 @@ struct cz_engine {
         for (size_t gi = 0; gi < groups.size(); gi++) {
             const Group &g = groups[gi];
             const uint32_t gn = g.fb - g.fa;
-            plan_segments(desc.data() + g.fa, gn, 0, SEG_BLOCKS, sg.seg, sg.comb, sg.npart);
+            uint64_t bs = g.slot0;
+            for (uint32_t i = g.fa; i < g.fb; i++) {
+                const OutMsg &m = pend[i];
+                Conn &c = conns[m.conn];
+                const uint64_t body = (uint64_t)m.len + CZ_MESSAGE_OVERHEAD;
+                h_desc[i] = {m.arena_off, bs, m.len, c.tx_key, c.nonce++, m.flags & 0xffu, -1};
+                h_items[i] = {bs, wpos[i], (uint32_t)body, (uint32_t)CZ_V2_ITEM_HEADER};
+                bs += round_up(body, SLOT_ALIGN);
+            }
+            plan_segments(h_desc + g.fa, gn, 0, SEG_BLOCKS, sg.seg, sg.comb, sg.npart);
             const uint32_t gseg = (uint32_t)sg.seg.size(), gcomb = (uint32_t)sg.comb.size();
-            memcpy(hm + m_seg + soff[gi] * sizeof(cz_segment), sg.seg.data(), (uint64_t)gseg * sizeof(cz_segment));
-            memcpy(hm + m_comb + coff[gi] * sizeof(cz_combine), sg.comb.data(), (uint64_t)gcomb * sizeof(cz_combine));
             if (gseg != soff[gi + 1] - soff[gi] || gcomb != coff[gi + 1] - coff[gi] || sg.npart != woff[gi + 1] - woff[gi])
                 return fail(CZ_EINVAL, "cz_engine: segment plan disagrees with its count");
+            memcpy(hm + m_seg + soff[gi] * sizeof(cz_segment), sg.seg.data(), (uint64_t)gseg * sizeof(cz_segment));
+            memcpy(hm + m_comb + coff[gi] * sizeof(cz_combine), sg.comb.data(), (uint64_t)gcomb * sizeof(cz_combine));
             cz_frame_desc *dd = (cz_frame_desc *)d_desc.ptr + g.fa;
             cz_segment *dsg = (cz_segment *)d_seg.ptr + soff[gi];
             cz_combine *dcb = (cz_combine *)d_comb.ptr + coff[gi];
             // (a) copy stream: the group's metadata, then the next group's arena bytes (copied while
-            //     the host plans that group)
-            if ((e = hipMemcpyAsync((cz_v2_item *)d_items.ptr + g.fa, (const cz_v2_item *)(hm + m_items) + g.fa,
-                                    (uint64_t)gn * sizeof(cz_v2_item), hipMemcpyHostToDevice, qh)) != hipSuccess ||
-                (e = hipMemcpyAsync(dd, (const cz_frame_desc *)(hm + m_desc) + g.fa, (uint64_t)gn * sizeof(cz_frame_desc),
+            //     the host builds that group)
+            if ((e = hipMemcpyAsync((cz_v2_item *)d_items.ptr + g.fa, h_items + g.fa, (uint64_t)gn * sizeof(cz_v2_item),
                                     hipMemcpyHostToDevice, qh)) != hipSuccess ||
+                (e = hipMemcpyAsync(dd, h_desc + g.fa, (uint64_t)gn * sizeof(cz_frame_desc), hipMemcpyHostToDevice,
+                                    qh)) != hipSuccess ||
                 (gseg && (e = hipMemcpyAsync(dsg, (const cz_segment *)(hm + m_seg) + soff[gi],
                                              (uint64_t)gseg * sizeof(cz_segment), hipMemcpyHostToDevice, qh)) !=
                              hipSuccess) ||

@@ -49,6 +49,8 @@ def parse():
                     help="zipf: input payload slot alignment in bytes (lengths are 64-byte multiples)")
     ap.add_argument("--out-align", type=int, default=128,
                     help="zipf: output slot alignment in bytes (the caller's packing choice)")
+    ap.add_argument("--plain-stride", type=int, default=0,
+                    help="open4k: plaintext slot stride in bytes (0 = the payload stride, 4096)")
     ap.add_argument("--config", default="4k", choices=["4k", "4k_dense", "100b", "zipf", "zipf_lane", "open4k", "e2e4k", "engine", "nacl",
                                                           "beforenm"])
     ap.add_argument("--frames", type=int, default=FRAMES)
@@ -122,7 +124,7 @@ def shard_plan(rank, frames_per_rank, cfg="4k"):
 class Workload:
     """Builds one rank's device-resident batch and the per-step launch."""
 
-    def __init__(self, cfg, frames, rank, dev, out_align=128, seg_blocks=128, in_align=64):
+    def __init__(self, cfg, frames, rank, dev, out_align=128, seg_blocks=128, in_align=64, plain_stride=0):
         self.cfg = cfg
         self.dev = dev
         key = torch.tensor(list(PRECOM), dtype=torch.uint8, device=dev).view(1, 32)
@@ -150,7 +152,9 @@ class Workload:
             if cfg == "open4k":
                 batch.seal_uniform(self.d_in, self.in_stride, self.d_out, self.out_stride, frames, n, self.subkey,
                                    self.counter0, flags8=self.flags)
-                self.d_plain = torch.empty_like(self.d_in)
+                # plaintext slots: the payload stride unless the caller pads them (--plain-stride)
+                self.plain_stride = plain_stride or self.in_stride
+                self.d_plain = torch.empty(frames * self.plain_stride, dtype=torch.uint8, device=dev)
                 self.status = torch.empty(frames, dtype=torch.int16, device=dev)
                 # open reads the body + writes payload + 2-byte status (+8 B prev nonce, L2-resident)
                 self.read_bytes = frames * (n + 33)
@@ -203,7 +207,7 @@ class Workload:
             batch.seal_uniform(self.d_in, self.in_stride, self.d_out, self.out_stride, self.count, self.n,
                                self.subkey, self.counter0, flags8=self.flags)
         elif self.cfg == "open4k":
-            batch.open_uniform(self.d_out, self.out_stride, self.d_plain, self.in_stride, self.count, self.n + 33,
+            batch.open_uniform(self.d_out, self.out_stride, self.d_plain, self.plain_stride, self.count, self.n + 33,
                                self.subkey, self.counter0 - 1, self.status)
         elif self.cfg == "zipf":
             batch.seal_segments(self.d_desc, self.plan, self.d_in, self.d_out, self.subkey.view(1, 32))
@@ -227,7 +231,8 @@ class Workload:
             st = self.status.cpu().numpy().view(np.uint16)
             if np.any(st & 0xff):
                 raise SystemExit("open failures in benchmark batch")
-            if not torch.equal(self.d_plain, self.d_in):
+            got = self.d_plain.view(self.count, self.plain_stride)[:, :self.n]
+            if not torch.equal(got, self.d_in.view(self.count, self.in_stride)[:, :self.n]):
                 raise SystemExit("open round trip mismatch")
         else:
             longest = int(np.argmax(self.desc_np["len"]))
@@ -723,7 +728,7 @@ def main():
             print(json.dumps(line), flush=True)
         return
     wl = Workload(args.config, args.frames, rank, dev, out_align=args.out_align, seg_blocks=args.seg_blocks,
-                  in_align=args.in_align)
+                  in_align=args.in_align, plain_stride=args.plain_stride)
 
     ramp = 0
     t_ramp = time.perf_counter()
@@ -810,7 +815,8 @@ def main():
             "data": "synthetic (SplitMix64 payload on device, RFC test keys)",
             "config": {"workload": names[args.config] + (
                            f", input offsets {args.in_align}-byte / output offsets {args.out_align}-byte aligned"
-                           if args.config.startswith("zipf") else ""),
+                           if args.config.startswith("zipf") else "") + (
+                           f", plaintext slots {wl.plain_stride} B" if args.config == "open4k" else ""),
                        "frames_per_gpu": wl.count,
                        "payload_bytes_per_gpu": wl.payload_bytes, "parallelism": f"shard{world}",
                        "frames_per_s": round(wl.count * world * args.steps / elapsed, 1)},

@@ -49,6 +49,10 @@ def parse():
                     help="zipf: input payload slot alignment in bytes (lengths are 64-byte multiples)")
     ap.add_argument("--out-align", type=int, default=128,
                     help="zipf: output slot alignment in bytes (the caller's packing choice)")
+    ap.add_argument("--in-stride", type=int, default=0,
+                    help="4k/100b/open4k: payload slot stride in bytes (0 = the payload size rounded to 16)")
+    ap.add_argument("--out-stride", type=int, default=0,
+                    help="4k/100b/open4k: body slot stride in bytes (0 = the config's own layout)")
     ap.add_argument("--plain-stride", type=int, default=0,
                     help="open4k: plaintext slot stride in bytes (0 = the payload stride, 4096)")
     ap.add_argument("--config", default="4k", choices=["4k", "4k_dense", "100b", "zipf", "zipf_lane", "open4k", "e2e4k", "engine", "nacl",
@@ -124,7 +128,8 @@ def shard_plan(rank, frames_per_rank, cfg="4k"):
 class Workload:
     """Builds one rank's device-resident batch and the per-step launch."""
 
-    def __init__(self, cfg, frames, rank, dev, out_align=128, seg_blocks=128, in_align=64, plain_stride=0):
+    def __init__(self, cfg, frames, rank, dev, out_align=128, seg_blocks=128, in_align=64, plain_stride=0,
+                 in_stride=0, out_stride=0):
         self.cfg = cfg
         self.dev = dev
         key = torch.tensor(list(PRECOM), dtype=torch.uint8, device=dev).view(1, 32)
@@ -140,6 +145,12 @@ class Workload:
             self.out_stride = (n + 33 + 127) // 128 * 128 if n >= 1024 else (n + 33 + 15) // 16 * 16
             if cfg == "4k_dense":  # bodies back to back (4129-byte slots), as the wire packs them
                 self.out_stride = n + 33
+            if in_stride:
+                assert in_stride >= n, "--in-stride below the payload size"
+                self.in_stride = in_stride
+            if out_stride:
+                assert out_stride >= n + 33, "--out-stride below the body size"
+                self.out_stride = out_stride
             self.d_in = torch.empty(frames * self.in_stride, dtype=torch.uint8, device=dev)
             batch.fill(self.d_in, seed)
             self.flags = torch.zeros(frames, dtype=torch.uint8, device=dev)
@@ -728,7 +739,8 @@ def main():
             print(json.dumps(line), flush=True)
         return
     wl = Workload(args.config, args.frames, rank, dev, out_align=args.out_align, seg_blocks=args.seg_blocks,
-                  in_align=args.in_align, plain_stride=args.plain_stride)
+                  in_align=args.in_align, plain_stride=args.plain_stride,
+                  in_stride=args.in_stride, out_stride=args.out_stride)
 
     ramp = 0
     t_ramp = time.perf_counter()
@@ -816,7 +828,9 @@ def main():
             "config": {"workload": names[args.config] + (
                            f", input offsets {args.in_align}-byte / output offsets {args.out_align}-byte aligned"
                            if args.config.startswith("zipf") else "") + (
-                           f", plaintext slots {wl.plain_stride} B" if args.config == "open4k" else ""),
+                           f", plaintext slots {wl.plain_stride} B" if args.config == "open4k" else "") + (
+                           f", slots in {wl.in_stride} / out {wl.out_stride} B"
+                           if args.in_stride or args.out_stride else ""),
                        "frames_per_gpu": wl.count,
                        "payload_bytes_per_gpu": wl.payload_bytes, "parallelism": f"shard{world}",
                        "frames_per_s": round(wl.count * world * args.steps / elapsed, 1)},

@@ -296,7 +296,7 @@ __device__ __forceinline__ void poly_block(Poly &P, u32 m0, u32 m1, u32 m2, u32 
 
     // propagate the column carries: h = d0 + d1*2^32 + d2*2^64 + d3*2^96 + h4r*2^128.
     // One v_addc_co_u32 per limb: lo(d_j) + hi(d_{j-1}) + carry < 2^32 + 2^30.3 + 1, so
-    // the carry out is 0 or 1; hi(d3) + h4r + carry < 2^31 does not carry.
+    // the carry out is 0 or 1; hi(d3) + h4r + carry < 2^31.1 does not carry (tests/test_poly_radix32.py).
     const u32 e0 = (u32)d0;
     const u32 e1 = addc((u32)d1, (u32)(d0 >> 32), 0u, c);
     const u32 e2 = addc((u32)d2, (u32)(d1 >> 32), c, c);

@@ -292,26 +292,27 @@ __device__ __forceinline__ void poly_block(Poly &P, u32 m0, u32 m1, u32 m2, u32 
     const u64 d1 = mad64(h4, P.s1, mad64(h3, P.s2, mad64(h2, P.s3, mad64(h1, P.r0, mad64(h0, P.r1, 0)))));
     const u64 d2 = mad64(h4, P.s2, mad64(h3, P.s3, mad64(h2, P.r0, mad64(h1, P.r1, mad64(h0, P.r2, 0)))));
     const u64 d3 = mad64(h4, P.s3, mad64(h3, P.r0, mad64(h2, P.r1, mad64(h1, P.r2, mad64(h0, P.r3, 0)))));
-    const u32 h4r = h4 * P.r0;
+    const u32 h4r = h4 * P.r0;  // the compiler fuses it with the add below (v_mad_u64_u32)
 
-    // propagate the column carries: h = d0 + d1*2^32 + d2*2^64 + d3*2^96 + h4r*2^128.
-    // One v_addc_co_u32 per limb: lo(d_j) + hi(d_{j-1}) + carry < 2^32 + 2^30.3 + 1, so
-    // the carry out is 0 or 1; hi(d3) + h4r + carry < 2^31.1 does not carry (tests/test_poly_radix32.py).
-    const u32 e0 = (u32)d0;
-    const u32 e1 = addc((u32)d1, (u32)(d0 >> 32), 0u, c);
-    const u32 e2 = addc((u32)d2, (u32)(d1 >> 32), c, c);
-    const u32 e3 = addc((u32)d3, (u32)(d2 >> 32), c, c);
-    const u32 e4 = addc((u32)(d3 >> 32), h4r, c, c);
-    // partial reduction, 2^130 == 5: fold e4's bits above 2^130 back in
-    const u32 q = e4 >> 2;
-    // k = 5q as one v_lshl_add_u32: left to itself the compiler emits (e4 & ~3) + q, two VALU
+    // h = d0 + d1*2^32 + d2*2^64 + d3*2^96 + h4r*2^128, partially reduced with 2^130 == 5 in
+    // ONE carry chain: the top word x = hi(d3) + h4r (< 2^30.4 + 2^30.6, no overflow) is split
+    // as 4q + (x & 3) before the column carries run, and 5q enters limb 0 with them:
+    //   h = (lo(d0) + 5q) + (lo(d1) + hi(d0))*2^32 + (lo(d2) + hi(d1))*2^64
+    //       + (lo(d3) + hi(d2))*2^96 + (x & 3)*2^128          (mod 2^130 - 5)
+    // Each step is a + b + carry < 2^33, one v_addc_co_u32 with carry 0 or 1; the chain's last
+    // carry lands in h4 <= 4, the same bound as folding after a separate column chain.  Bounds
+    // and exactness: tests/test_poly_radix32.py.  Against the two-chain form: 17 VALU fewer per
+    // 128-byte block pair in the 4k seal loop (1961 -> 1944).
+    const u32 x = (u32)(d3 >> 32) + h4r;
+    const u32 q = x >> 2;
+    // k = 5q as one v_lshl_add_u32: left to itself the compiler emits (x & ~3) + q, two VALU
     u32 k;
     asm("v_lshl_add_u32 %0, %1, 2, %1" : "=v"(k) : "v"(q));
-    P.h0 = addc(e0, k, 0u, c);
-    P.h1 = addc(e1, 0u, c, c);
-    P.h2 = addc(e2, 0u, c, c);
-    P.h3 = addc(e3, 0u, c, c);
-    P.h4 = (e4 & 3u) + c;
+    P.h0 = addc((u32)d0, k, 0u, c);
+    P.h1 = addc((u32)d1, (u32)(d0 >> 32), c, c);
+    P.h2 = addc((u32)d2, (u32)(d1 >> 32), c, c);
+    P.h3 = addc((u32)d3, (u32)(d2 >> 32), c, c);
+    P.h4 = (x & 3u) + c;
 }
 
 // Final block of len bytes (1..15): bytes >= len cleared, byte len = 0x01, no 2^128 bit.

@@ -353,7 +353,13 @@ struct EmitLines {
             {
                 typedef unsigned v4u __attribute__((ext_vector_type(4)));
                 const v4u d = {v.x, v.y, v.z, v.w};
-                asm volatile("global_store_dwordx4 %0, %1, %2 " CZ_DIAG_STORE_POLICY ::"v"(voff), "v"(d), "s"(p)
+                // s_nop 0: a store with more than 64 bits of data reads its data VGPRs after issue,
+                // and a VALU that rewrites them must wait one state.  The compiler inserts that wait
+                // for its own stores but not after an asm one: with a store last in the flush and a
+                // v_mad_u64_u32 of the open's Poly1305 writing d.x next, lanes 12-15 of each 16-lane
+                // pass stored the new value.
+                asm volatile("global_store_dwordx4 %0, %1, %2 " CZ_DIAG_STORE_POLICY "\n\ts_nop 0"
+                             ::"v"(voff), "v"(d), "s"(p)
                              : "memory");
             }
 #endif

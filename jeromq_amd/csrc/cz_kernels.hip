@@ -358,9 +358,18 @@ struct EmitLines {
                 // for its own stores but not after an asm one: with a store last in the flush and a
                 // v_mad_u64_u32 of the open's Poly1305 writing d.x next, lanes 12-15 of each 16-lane
                 // pass stored the new value.
-                asm volatile("global_store_dwordx4 %0, %1, %2 " CZ_DIAG_STORE_POLICY "\n\ts_nop 0"
-                             ::"v"(voff), "v"(d), "s"(p)
-                             : "memory");
+                // s_nop 4 before the first store: a VMEM instruction reading an SGPR that a VALU
+                // wrote (the v_readfirstlane line base above) needs 5 wait states, which the
+                // compiler does not count into an asm statement either.  The later stores' base
+                // comes from scalar adds.
+                if (j == 0)
+                    asm volatile("s_nop 4\n\tglobal_store_dwordx4 %0, %1, %2 " CZ_DIAG_STORE_POLICY "\n\ts_nop 0"
+                                 ::"v"(voff), "v"(d), "s"(p)
+                                 : "memory");
+                else
+                    asm volatile("global_store_dwordx4 %0, %1, %2 " CZ_DIAG_STORE_POLICY "\n\ts_nop 0"
+                                 ::"v"(voff), "v"(d), "s"(p)
+                                 : "memory");
             }
 #endif
             p += step;

@@ -1,62 +1,79 @@
-"""Scan a hipcc --save-temps .s for two VMEM hazards the compiler does not count into inline asm.
-(1) store data: a global_store_dwordx4 whose data
-VGPRs a VALU rewrites within the next two instructions (one intervening instruction or an
-s_nop is the required wait state; distance 1 is the hazard); (2) a VALU-written SGPR read as a VMEM
-address needs 5 wait states.  usage: python tools/isa_store_hazard.py file.s"""
-import re,sys
-lines=open(sys.argv[1]).read().splitlines()
-cur=None; hits=0; total=0; ex=[]; allx=[]
-def regs(tok):
-    m=re.match(r"v\[(\d+):(\d+)\]",tok)
-    if m: return set(range(int(m.group(1)),int(m.group(2))+1))
-    m=re.match(r"v(\d+)$",tok)
-    return {int(m.group(1))} if m else set()
-for i,l in enumerate(lines):
-    t=l.strip()
-    if t.startswith("global_store_dwordx4"):
-        ops=[o.strip() for o in t.split(None,1)[1].split(",")]
-        data=regs(ops[1]); total+=1
-        # next real instructions
-        k=i+1; seen=0
-        while k<len(lines) and seen<2:
-            u=lines[k].strip(); k+=1
-            if not u or u.startswith((";",".")): continue
-            seen+=1
-            op=u.split()[0]
-            if op.startswith("s_nop"): break
-            if op.startswith("v_"):
-                dst=u.split(None,1)[1].split(",")[0].strip()
-                if regs(dst)&data:
-                    hits+=1
-                    allx.append((i,t,u,seen))
-                    if len(ex)<5: ex.append((i,t,u,seen))
-print("stores", total, "VALU overwrites of store data at distance 2 (safe):", sum(1 for e in allx if e[3] == 2),
-      "at distance 1 (HAZARD):", sum(1 for e in allx if e[3] == 1))
-for e in allx:
-    if e[3] == 1:
-        print("hazard:", e)
+"""Scan a gfx950 ISA listing (hipcc --save-temps .s, or --cuda-device-only -S) for two VMEM hazards
+that the compiler counts for its own instructions but not into inline asm (EmitLines::flush stores
+through an asm global_store_dwordx4):
 
-# second check: a VALU-written SGPR (v_readfirstlane) read as a VMEM address within 5 wait states
-L=[l.strip() for l in open(sys.argv[1]).read().splitlines()]
-ins=[l for l in L if l and not l.startswith((";",".")) and not re.match(r"^\S+:",l)]
-bad=0
-for i,t in enumerate(ins):
-    op=t.split()[0]
-    if not (op.startswith("global_") or op.startswith("buffer_") or op.startswith("flat_")): continue
-    m=re.search(r"s\[(\d+):(\d+)\]",t)
-    if not m: continue
-    sg={int(m.group(1)),int(m.group(2))}
-    ws=0
-    for k in range(i-1,max(-1,i-8),-1):
-        u=ins[k]; o=u.split()[0]
-        if o.startswith("s_nop"):
-            ws+=int(u.split()[1])+1; continue
-        if o.startswith("v_") :
-            d=u.split(None,1)[1].split(",")[0].strip()
-            mm=re.match(r"s(\d+)$",d) or re.match(r"s\[(\d+):(\d+)\]",d)
-            if mm and (set(int(x) for x in mm.groups() if x)&sg) and ws<5:
-                bad+=1
-                if bad<=5: print("VALU-SGPR -> VMEM within",ws,"states:",u,"|",t)
+  (1) store data: a store with more than 64 bits of data reads its data VGPRs after issue; a VALU
+      that rewrites them must wait one state (distance 1 = hazard, one instruction or s_nop between
+      = safe);
+  (2) a VMEM instruction reading an SGPR (its saddr) that a VALU wrote (v_readfirstlane) needs 5
+      wait states.
+
+The scan is linear over the text (it ignores branches), so it may over-report, never under-report
+a straight-line case.  usage: python tools/isa_store_hazard.py file.s"""
+import re
+import sys
+
+
+def _vregs(tok):
+    m = re.match(r"v\[(\d+):(\d+)\]", tok)
+    if m:
+        return set(range(int(m.group(1)), int(m.group(2)) + 1))
+    m = re.match(r"v(\d+)$", tok)
+    return {int(m.group(1))} if m else set()
+
+
+def _instrs(text):
+    out = []
+    for line in text.splitlines():
+        t = line.strip()
+        if not t or t.startswith((";", ".")) or re.match(r"^\S+:", t):
+            continue
+        out.append(t)
+    return out
+
+
+def scan(text):
+    """-> (store-data hazards, VALU-SGPR -> VMEM hazards): lists of (store, offending instruction)."""
+    ins = _instrs(text)
+    data_hz, sgpr_hz = [], []
+    for i, t in enumerate(ins):
+        op = t.split()[0]
+        if not op.startswith(("global_", "buffer_", "flat_")):
+            continue
+        ops = [o.strip() for o in t.split(None, 1)[1].split(",")] if " " in t else []
+        if op.startswith(("global_store_dwordx", "buffer_store_dwordx", "flat_store_dwordx")) and len(ops) > 1:
+            data = _vregs(ops[1])
+            if len(data) > 2 and i + 1 < len(ins):  # > 64 bits of store data
+                u = ins[i + 1]
+                if u.startswith("v_") and " " in u and _vregs(u.split(None, 1)[1].split(",")[0].strip()) & data:
+                    data_hz.append((t, u))
+        m = re.search(r"s\[(\d+):(\d+)\]", t)
+        if not m:
+            continue
+        sg = {int(m.group(1)), int(m.group(2))}
+        ws = 0
+        for k in range(i - 1, max(-1, i - 8), -1):
+            u = ins[k]
+            o = u.split()[0]
+            if o == "s_nop":
+                ws += int(u.split()[1], 0) + 1
+                continue
+            if o.startswith("v_") and " " in u:
+                d = u.split(None, 1)[1].split(",")[0].strip()
+                mm = re.match(r"s(\d+)$", d) or re.match(r"s\[(\d+):(\d+)\]", d)
+                if mm and {int(x) for x in mm.groups() if x} & sg and ws < 5:
+                    sgpr_hz.append((t, u))
+                    break
+            ws += 1
+            if ws >= 5:
                 break
-        ws+=1
-print("VALU-written SGPR used as VMEM address within 5 states:",bad)
+    return data_hz, sgpr_hz
+
+
+if __name__ == "__main__":
+    d, s = scan(open(sys.argv[1]).read())
+    print("store-data hazards (VALU rewrites store data at distance 1):", len(d))
+    print("VALU-written SGPR read as a VMEM address within 5 wait states:", len(s))
+    for h in (d + s)[:10]:
+        print("  ", h)
+    sys.exit(1 if d or s else 0)

@@ -105,6 +105,18 @@ struct __attribute__((packed)) U16ua {
     uint4 v;
 };
 
+// Stores through pointers rebuilt from integers (ds_bpermute'd bases, SGPR line bases) would
+// compile to flat_* instructions, which also count against lgkmcnt: every LDS wait of an
+// emitter would then wait for them too.  These go out as global_* stores.
+typedef unsigned v4u_t __attribute__((ext_vector_type(4)));
+typedef __attribute__((address_space(1))) v4u_t g_uint4;
+typedef __attribute__((address_space(1))) uint8_t g_u8;
+typedef __attribute__((address_space(1))) u64_ua g_u64_ua;
+typedef __attribute__((address_space(1))) u32_ua g_u32_ua;
+typedef __attribute__((address_space(1))) u16_ua g_u16_ua;
+typedef v4u_t v4u_ua __attribute__((aligned(1)));
+typedef __attribute__((address_space(1))) v4u_ua g_v4u_ua;
+
 // store bytes [a, b) (0 <= a <= b <= 16) of the unit v whose byte 0 belongs at p
 __device__ void st_range16(uint8_t *p, uint4 v, u32 a, u32 b)
 {
@@ -316,16 +328,24 @@ struct EmitLines {
         uint8_t *p = wbase + 128u * r + 16u * c;  // every line of the wave onto its first 8 KiB
         const u64 step = 1024u;  // (diagnostic build: plain stores)
 #else
-        // wave-uniform line base in SGPRs, advanced by the scalar unit, plus a per-lane 32-bit
-        // offset: saddr stores with no 64-bit VALU address arithmetic per store
+        // A buffer store: the line's wave-uniform base in the resource (SGPRs, rebuilt by the
+        // scalar unit per line), this lane's 32-bit offset in a VGPR computed once, and the
+        // j-th frame group's offset j * 8 * stride as the SGPR soffset -- no VALU address
+        // arithmetic at all per store (plain C stores cost a v_lshl_add_u64 each, +8 VALU and
+        // 16 VGPRs per block pair).  It is a compiler builtin, not inline asm, so the backend
+        // counts the store's wait states itself (round 2's asm store was outside its hazard
+        // recognizer, and a rescheduled Poly1305 v_mad_u64_u32 rewrote one store's data VGPRs
+        // one state after issue: DESIGN.md section 6).  The launcher keeps 64 * stride < 2^31.
         const u64 wb = (u64)(uintptr_t)wbase;
         // (readfirstlane returns int: each half goes through u32 before widening, or a low half
         // with bit 31 set would sign-extend over the high one)
-        u64 p = (((u64)(u32)__builtin_amdgcn_readfirstlane((u32)(wb >> 32)) << 32) |
-                 (u64)(u32)__builtin_amdgcn_readfirstlane((u32)wb)) +
-                128ull * line;
+        const u64 lb = (((u64)(u32)__builtin_amdgcn_readfirstlane((u32)(wb >> 32)) << 32) |
+                        (u64)(u32)__builtin_amdgcn_readfirstlane((u32)wb)) +
+                       128ull * line;
+        const __amdgpu_buffer_rsrc_t rs =
+            __builtin_amdgcn_make_buffer_rsrc(reinterpret_cast<void *>((uintptr_t)lb), 0, (int)0xffffffffu, 0x00020000);
         const u32 voff = r * (u32)stride + 16u * c;
-        const u64 step = 8ull * stride;
+        const u32 step = 8u * (u32)stride;
 #endif
 #ifdef CZ_DIAG_NOTAG
         const bool skip = false;
@@ -344,35 +364,14 @@ struct EmitLines {
 #else
             if (!skip)
 #endif
-#ifndef CZ_DIAG_STORE_POLICY  // cache-policy bits on the line stores, e.g. -DCZ_DIAG_STORE_POLICY='"sc1"'
-#define CZ_DIAG_STORE_POLICY ""
-#endif
 #ifdef CZ_DIAG_L2STORE
-                *reinterpret_cast<uint4 *>(p) = v;
-#else
             {
-                typedef unsigned v4u __attribute__((ext_vector_type(4)));
-                const v4u d = {v.x, v.y, v.z, v.w};
-                // s_nop 0: a store with more than 64 bits of data reads its data VGPRs after issue,
-                // and a VALU that rewrites them must wait one state.  The compiler inserts that wait
-                // for its own stores but not after an asm one: with a store last in the flush and a
-                // v_mad_u64_u32 of the open's Poly1305 writing d.x next, lanes 12-15 of each 16-lane
-                // pass stored the new value.
-                // s_nop 4 before the first store: a VMEM instruction reading an SGPR that a VALU
-                // wrote (the v_readfirstlane line base above) needs 5 wait states, which the
-                // compiler does not count into an asm statement either.  The later stores' base
-                // comes from scalar adds.
-                if (j == 0)
-                    asm volatile("s_nop 4\n\tglobal_store_dwordx4 %0, %1, %2 " CZ_DIAG_STORE_POLICY "\n\ts_nop 0"
-                                 ::"v"(voff), "v"(d), "s"(p)
-                                 : "memory");
-                else
-                    asm volatile("global_store_dwordx4 %0, %1, %2 " CZ_DIAG_STORE_POLICY "\n\ts_nop 0"
-                                 ::"v"(voff), "v"(d), "s"(p)
-                                 : "memory");
+                *reinterpret_cast<uint4 *>(p) = v;
             }
-#endif
             p += step;
+#else
+                __builtin_amdgcn_raw_buffer_store_b128(v4u_t{v.x, v.y, v.z, v.w}, rs, (int)voff, (int)(j * step), 0);
+#endif
         }
     }
     __device__ __forceinline__ void emit(u32 q, const u32 Din[16])
@@ -1070,18 +1069,6 @@ __device__ __forceinline__ u64 read_be64(const uint8_t *p)
 // at the loop's convergence point, so a wave whose lanes hold segments with
 // the same chunk count can share the cooperative line emitter below.
 // ---------------------------------------------------------------------------
-
-// Stores through pointers rebuilt from integers (ds_bpermute'd bases) would compile to flat_*
-// instructions, which also count against lgkmcnt: every LDS wait of the emitter would then
-// wait for them too.  These go out as global_* stores.
-typedef unsigned v4u_t __attribute__((ext_vector_type(4)));
-typedef __attribute__((address_space(1))) v4u_t g_uint4;
-typedef __attribute__((address_space(1))) uint8_t g_u8;
-typedef __attribute__((address_space(1))) u64_ua g_u64_ua;
-typedef __attribute__((address_space(1))) u32_ua g_u32_ua;
-typedef __attribute__((address_space(1))) u16_ua g_u16_ua;
-typedef v4u_t v4u_ua __attribute__((aligned(1)));
-typedef __attribute__((address_space(1))) v4u_ua g_v4u_ua;
 
 // bytes [a, b) of unit v at global address p (st_range16 for a global pointer); out of line:
 // only an output's edge units take it
@@ -2480,7 +2467,8 @@ int pick_staging(uint64_t stride, uint32_t out_bytes, bool aligned)
 {
     if (!aligned)
         return ST_DIRECT;
-    if (stride % 128 == 0 && out_bytes >= 256 && stride <= 0xffffffffull)
+    // (EmitLines' buffer-store offsets, up to 64 * stride, stay below 2^31)
+    if (stride % 128 == 0 && out_bytes >= 256 && stride < (1ull << 25))
         return ST_LINES;
     if (stride % 16 == 0 && 64 * stride <= REGION_MAX)
         return ST_REGION;

@@ -215,6 +215,17 @@ struct cz_engine {
     HostBuf h_meta;  // pinned staging of descriptors / items / segment lists (async H2D)
     RxPool rxpool;   // every connection's receive buffer
 
+    // wait for everything issued on every stream (error paths of the flushes: the next recv /
+    // flush may write or regrow the pinned buffers those copies still read or write)
+    void drain()
+    {
+        if (stream)
+            (void)hipStreamSynchronize(stream);
+        for (hipStream_t q : ps)
+            if (q)
+                (void)hipStreamSynchronize(q);
+    }
+
     ~cz_engine()
     {
         if (stream) {
@@ -918,7 +929,10 @@ int cz_engine_flush_out(cz_engine *e)
     hipError_t he = hipSetDevice(e->device);
     if (he != hipSuccess)
         return hip_fail(he, "hipSetDevice");
-    return e->flush_out();
+    const int rc = e->flush_out();
+    if (rc != CZ_OK)
+        e->drain();  // an error return may leave copies into/out of the pinned buffers in flight
+    return rc;
 }
 
 int cz_engine_wire_out(cz_engine *e, int conn, const uint8_t **wire, uint64_t *len)
@@ -1021,7 +1035,10 @@ int cz_engine_flush_in(cz_engine *e)
     hipError_t he = hipSetDevice(e->device);
     if (he != hipSuccess)
         return hip_fail(he, "hipSetDevice");
-    return e->flush_in();
+    const int rc = e->flush_in();
+    if (rc != CZ_OK)
+        e->drain();  // an error return may leave copies into/out of the pinned buffers in flight
+    return rc;
 }
 
 int cz_engine_msgs_in(cz_engine *e, int conn, uint32_t *count)

@@ -175,6 +175,47 @@ def test_client_failure_events(hs):
     assert cli.last_event == 0x10000015
 
 
+def test_client_rejects_out_of_order_welcome_and_ready(hs):
+    """Stricter than CurveClientMechanism.java:108-129 on purpose (the reference dispatches on the
+    command name in any state): a READY before any WELCOME would open under the all-zero cnPrecom
+    and hand the engine that key; a WELCOME after CONNECTED would re-key the session.  Both are
+    UNEXPECTED_COMMAND, the state is unchanged and no session is handed out."""
+    c = S["client_handshake"]
+    mk = lambda: hs.CurveClientHandshake(CLIENT_PUB, CLIENT_SEC, SERVER_PUB,  # noqa: E731
+                                         ephemeral_secret=H(S["client_ephemeral_secret"]),
+                                         entropy=H(c["vouch_nonce"]))
+    # a READY sealed under the all-zero key, before the HELLO and after it
+    from cz_testlib import oracle
+    import ctypes
+    rm = bytes(32) + b"\x0bSocket-Type\x00\x00\x00\x04PAIR"
+    nonce = b"CurveZMQREADY---" + (1).to_bytes(8, "big")
+    box = ctypes.create_string_buffer(len(rm))
+    assert oracle().or_secretbox(box, rm, len(rm), nonce, bytes(32)) == 0
+    forged = b"\x05READY" + nonce[16:] + box.raw[16:]
+    for sent_hello in (False, True):
+        cli = mk()
+        if sent_hello:
+            cli.nextHandshakeCommand()
+        assert cli.processHandshakeCommand(forged) == hs.EPROTO
+        assert cli.last_event == 0x10000001                               # UNEXPECTED_COMMAND
+        assert cli.status() == hs.Status.HANDSHAKING
+        with pytest.raises(Exception):
+            cli.session()
+    # the recorded READY while still expecting the WELCOME
+    cli = mk()
+    cli.nextHandshakeCommand()
+    assert cli.processHandshakeCommand(H(c["ready"])) == hs.EPROTO and cli.last_event == 0x10000001
+    # a second WELCOME after the handshake completed does not re-key
+    cli = mk()
+    cli.nextHandshakeCommand()
+    assert cli.processHandshakeCommand(H(c["welcome"])) == 0
+    cli.nextHandshakeCommand()
+    assert cli.processHandshakeCommand(H(c["ready"])) == 0 and cli.status() == hs.Status.READY
+    before = cli.session()
+    assert cli.processHandshakeCommand(H(c["welcome"])) == hs.EPROTO and cli.last_event == 0x10000001
+    assert cli.status() == hs.Status.READY and cli.session() == before
+
+
 def test_server_failure_events(hs):
     s = S["server_session"]
     mk = lambda **kw: hs.CurveServerHandshake(SERVER_SEC, ephemeral_secret=H(s["server_ephemeral_secret"]),  # noqa

@@ -105,6 +105,7 @@ SIGNATURES = {
     "cz_seal_segments": (_I, [_VP, _VP, _U32, _VP, _U32, _VP, _VP, _VP, _VP, _VP]),
     "cz_open_segments": (_I, [_VP, _VP, _U32, _VP, _U32, _VP, _VP, _VP, _VP, _VP, _VP, _VP]),
     "cz_fill": (_I, [_VP, _U64, _U64, _VP]),
+    "cz_dev_copy": (_I, [_VP, _VP, _U64, _VP]),
     "cz_ctx_create": (_I, [ctypes.POINTER(_VP), _I]),
     "cz_ctx_destroy": (None, [_VP]),
     "cz_ctx_set_keys": (_I, [_VP, _VP, _U32, _I]),
@@ -183,7 +184,10 @@ def lib():
         raise CzError(f"{LIB_PATH} is missing: run `python -m jeromq_amd.build` (hipcc, gfx950). "
                       "There is no CPU fallback for the CURVE path.")
     L = ctypes.CDLL(LIB_PATH)
+    ab_variant = "CZ_LIB" in os.environ  # an older A/B build may predate a symbol; the product may not
     for name, (res, args) in SIGNATURES.items():
+        if ab_variant and not hasattr(L, name):
+            continue
         f = getattr(L, name)
         f.restype = res
         f.argtypes = args

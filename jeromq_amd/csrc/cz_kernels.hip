@@ -1155,7 +1155,13 @@ __device__ void zero_bytes(uint8_t *p, u32 n)
 constexpr u32 SROW = 208;  // 16 headroom + 192 bytes used; 52 dwords apart: conflict-free 16-lane b128
 constexpr u32 SHIFT_LDS_BYTES = 64 * SROW;  // EmitShiftLines: 13 KiB per wave
 constexpr u32 SHEAD = 16;  // row bytes before line-space byte 0 (a chunk's first dword may start 4 early)
-struct EmitShiftLines {
+// UNI (uniform batches: output i at out + i * stride): every lane fetches, once per frame, the
+// workgroup-relative frame index of the 8 outputs it stores for (ds_bpermute) and keeps their
+// 128-byte line offsets from the workgroup's line-aligned base in 8 VGPRs, so the interior-line
+// flush -- the hot one -- is 8 ds_read_b128 + 8 buffer stores with no per-store ds_bpermute and
+// no VALU address arithmetic (the base lives in the SGPR resource, the line in soffset).
+template <bool UNI>
+struct EmitShiftLinesT {
     static constexpr bool cooperative = true;
     uint8_t *rows;   // this wave's 64 rows of SROW bytes
     uint8_t *mine;
@@ -1164,6 +1170,25 @@ struct EmitShiftLines {
     u32 mixed;       // the wave holds outputs of both classes
     u32 carry_w;     // the previous chunk's last dword (the first shifted dword of a chunk straddles both)
     u32 walign;      // largest of 16 / 8 / 1 that divides every output's line offset in the wave
+    u64 ubase;       // UNI: the workgroup's first output address rounded down to 128 (wave-uniform)
+    u32 loff[8];     // UNI: line offset from ubase of output F = 8j + lane / 8, plus 16 * (lane & 7)
+
+    // UNI: rel = this lane's workgroup-relative frame index, wg_out = the workgroup's frame-0 output
+    // (the launcher keeps 256 * stride + the output length below 2^31)
+    __device__ __forceinline__ void init_uniform(u32 rel, u32 stride, const uint8_t *wg_out)
+    {
+        const u64 wo = (u64)(uintptr_t)wg_out;
+        const u64 wu = ((u64)(u32)__builtin_amdgcn_readfirstlane((u32)(wo >> 32)) << 32) |
+                       (u64)(u32)__builtin_amdgcn_readfirstlane((u32)wo);
+        ubase = wu & ~(u64)127;
+        const u32 a = (u32)wu & 127u;
+        const u32 c = lane & 7u, r = lane >> 3;
+#pragma unroll
+        for (u32 j = 0; j < 8; j++) {
+            const u32 relF = (u32)__builtin_amdgcn_ds_bpermute((int)((8u * j + r) << 2), (int)rel);
+            loff[j] = ((a + relF * stride) & ~127u) + 16u * c;
+        }
+    }
 
     // the launchers keep d + total below 2^31
     __device__ __forceinline__ void init(bool tag_slot)
@@ -1194,7 +1219,21 @@ struct EmitShiftLines {
             // tag slot, whole before the output's end): unclipped stores, only the base fetched.
             const u32 k = q >> 1;
             const bool inner = k >= 2u && 128u * (k + 1u) <= (te & 0x7fffffffu);
-            if (__builtin_amdgcn_ballot_w64(!inner) == 0) {
+            if constexpr (UNI) {
+                if (__builtin_amdgcn_ballot_w64(!inner) == 0) {
+                    const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(
+                        reinterpret_cast<void *>((uintptr_t)ubase), 0, (int)0xffffffffu, 0x00020000);
+                    const u32 so = (u32)__builtin_amdgcn_readfirstlane(128u * k);
+#pragma unroll
+                    for (u32 j = 0; j < 8; j++) {
+                        const u32 F = 8u * j + r;
+                        const uint4 v = *reinterpret_cast<const uint4 *>(rows + F * SROW + SHEAD + 16u * c);
+                        __builtin_amdgcn_raw_buffer_store_b128(v4u_t{v.x, v.y, v.z, v.w}, rs, (int)loff[j], (int)so, 0);
+                    }
+                    return;
+                }
+            }
+            if (!UNI && __builtin_amdgcn_ballot_w64(!inner) == 0) {
 #pragma unroll
                 for (u32 j = 0; j < 8; j++) {
                     const u32 F = 8u * j + r;
@@ -1323,6 +1362,8 @@ struct EmitShiftLines {
         zero_bytes(mine, total);
     }
 };
+using EmitShiftLines = EmitShiftLinesT<false>;
+using EmitShiftLinesUni = EmitShiftLinesT<true>;
 
 // Line staging for a wave of segments at arbitrary 16-byte aligned bases.  Like
 // EmitLines, 8 lanes write one 128-byte output line per store instruction, but
@@ -1410,9 +1451,12 @@ struct EmitSegLines {
 // instead of at every chunk.  `cls` is the class of this thread's own item; returns the
 // workgroup-relative index of the item this thread takes instead.  Deterministic (a
 // stable partition), so kernels that split waves between them agree on the layout.
-__device__ __forceinline__ u32 class_permute(bool cls)
+// perm: BLOCK + WAVES words of scratch LDS, free again on return.  The kernels pass the start of
+// their dynamic LDS (the emitter rows, not in use yet): a static array of its own would add
+// 1040 bytes per workgroup, and 3 x (52 KiB rows + that) no longer fit a CU's 160 KiB -- the
+// dense seal then ran 2 waves per SIMD instead of 3.
+__device__ __forceinline__ u32 class_permute(bool cls, u32 *__restrict__ perm)
 {
-    __shared__ u32 perm[BLOCK + WAVES];
     const u32 tid = threadIdx.x, w = tid >> 6;
     const uint64_t m = __builtin_amdgcn_ballot_w64(cls);
     const u32 below1 = __builtin_amdgcn_mbcnt_hi((u32)(m >> 32), __builtin_amdgcn_mbcnt_lo((u32)m, 0u));
@@ -1836,7 +1880,8 @@ __global__ __launch_bounds__(BLOCK) CZ_OCC void k_seal_uniform(const uint8_t *__
     if constexpr (ST == ST_SHIFT) {
         // waves of one line phase (EmitShiftLines): a full workgroup's frames sorted by class
         if (blockIdx.x * BLOCK + BLOCK <= count)
-            i = blockIdx.x * BLOCK + class_permute(((uintptr_t)(out + (uint64_t)i * out_stride) & 64u) != 0);
+            i = blockIdx.x * BLOCK + class_permute(((uintptr_t)(out + (uint64_t)i * out_stride) & 64u) != 0,
+                                                   reinterpret_cast<u32 *>(smem));
     }
     const uint32_t wave_first = (blockIdx.x * BLOCK + threadIdx.x) & ~63u;
     if (wave_first >= count)
@@ -1862,13 +1907,14 @@ __global__ __launch_bounds__(BLOCK) CZ_OCC void k_seal_uniform(const uint8_t *__
                 seal_frame<MODE_ZMQ, true, EmitLines, PAIR, false>(src, len, fl, counter0 + i, key, em);
         } else if constexpr (ST == ST_SHIFT) {
             // bodies at any byte offset (dense packing, wire layout): byte-shifted line staging
-            EmitShiftLines em{reinterpret_cast<uint8_t *>(smem) + (threadIdx.x >> 6) * SHIFT_LDS_BYTES, dst, lane,
-                              mlen, 0u, 0u};
+            EmitShiftLinesUni em{reinterpret_cast<uint8_t *>(smem) + (threadIdx.x >> 6) * SHIFT_LDS_BYTES, dst, lane,
+                                 mlen, 0u, 0u};
             em.init(true);
+            em.init_uniform(i - blockIdx.x * BLOCK, (u32)out_stride, out + (uint64_t)blockIdx.x * BLOCK * out_stride);
             if (un0)
-                seal_frame<MODE_ZMQ, true, EmitShiftLines, PAIR, true>(src, len, fl, counter0 + i, key, em);
+                seal_frame<MODE_ZMQ, true, EmitShiftLinesUni, PAIR, true>(src, len, fl, counter0 + i, key, em);
             else
-                seal_frame<MODE_ZMQ, true, EmitShiftLines, PAIR, false>(src, len, fl, counter0 + i, key, em);
+                seal_frame<MODE_ZMQ, true, EmitShiftLinesUni, PAIR, false>(src, len, fl, counter0 + i, key, em);
         } else {
             const u32 st = (u32)out_stride;
             EmitRegion em{smem + (threadIdx.x >> 6) * ((64u * st) >> 4), out + (uint64_t)wave_first * out_stride, st,
@@ -2462,6 +2508,23 @@ __global__ __launch_bounds__(BLOCK) void k_fill(uint8_t *__restrict__ buf, uint6
     }
 }
 
+// Device-to-device copy, 16-byte loads and stores, 4 in flight per thread (bench.py's HBM copy
+// ceiling: the float4 copy of the MI355X guide)
+__global__ __launch_bounds__(BLOCK) void k_copy16(uint4 *__restrict__ dst, const uint4 *__restrict__ src, uint64_t n16)
+{
+    const uint64_t stride = (uint64_t)gridDim.x * BLOCK;
+    uint64_t i = (uint64_t)blockIdx.x * BLOCK + threadIdx.x;
+    for (; i + 3 * stride < n16; i += 4 * stride) {
+        const uint4 a = src[i], b = src[i + stride], c = src[i + 2 * stride], d = src[i + 3 * stride];
+        dst[i] = a;
+        dst[i + stride] = b;
+        dst[i + 2 * stride] = c;
+        dst[i + 3 * stride] = d;
+    }
+    for (; i < n16; i += stride)
+        dst[i] = src[i];
+}
+
 // Staging choice for a uniform batch (all pointers 16-byte aligned assumed by the caller check).
 int pick_staging(uint64_t stride, uint32_t out_bytes, bool aligned)
 {
@@ -2503,7 +2566,8 @@ hipError_t czk_seal_uniform(const void *in, uint64_t in_stride, void *out, uint6
                        (uint8_t *)out, out_stride, count, len, (const uint8_t *)subkey, counter0, flags8, g_un0)
     int st = pick_staging(out_stride, len + 33u, al);
     // bodies at any byte offset (dense slots, wire layout) from aligned payloads: shifted line staging
-    if (st == ST_DIRECT && in_al && len + 33u >= 256u && len < 0x7fffff00u && g_shift)
+    // (EmitShiftLinesUni's buffer-store offsets, below 256 * stride + len + 160, stay below 2^31)
+    if (st == ST_DIRECT && in_al && len + 33u >= 256u && out_stride < (1ull << 22) && len < (1u << 29) && g_shift)
         st = ST_SHIFT;
     const unsigned lds = st == ST_LINES ? WAVES * (LINE_LDS_BYTES + HOLD_LDS_BYTES)
                                         : st == ST_SHIFT ? WAVES * SHIFT_LDS_BYTES
@@ -2668,6 +2732,17 @@ int czk_tune(const char *key, int value)
         return old;
     }
     return -1;
+}
+
+hipError_t czk_copy16(void *dst, const void *src, uint64_t nbytes, hipStream_t s)
+{
+    const uint64_t n16 = nbytes / 16;
+    if (n16 == 0)
+        return hipSuccess;
+    const uint64_t want = (n16 + 4 * BLOCK - 1) / (4 * BLOCK);
+    const unsigned blocks = (unsigned)(want < 256 * 16 ? want : 256 * 16);  // 16 workgroups per CU
+    hipLaunchKernelGGL(k_copy16, dim3(blocks), dim3(BLOCK), 0, s, (uint4 *)dst, (const uint4 *)src, n16);
+    return hipGetLastError();
 }
 
 hipError_t czk_fill(void *buf, uint64_t nbytes, uint64_t seed, hipStream_t s)

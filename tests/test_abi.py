@@ -107,7 +107,9 @@ def test_argument_validation(lib):
 
 def test_plan_segments_orders_by_length_then_line_phase(lib):
     """cz_plan_segments (host): longest first; within one length, segments whose input starts on
-    a 128-byte line before those starting 64 bytes into one (seal), so waves hold one phase."""
+    a 128-byte line before those starting 64 bytes into one (seal), so waves hold one phase; then
+    by the output's line class (bit 6 of its offset), so waves of outputs packed at any byte offset
+    hold one EmitShiftLines class."""
     import numpy as np
     from jeromq_amd.batch import DESC_DTYPE, SegmentPlan
     rng = np.random.default_rng(3)
@@ -115,13 +117,16 @@ def test_plan_segments_orders_by_length_then_line_phase(lib):
     d = np.zeros(len(lens), dtype=DESC_DTYPE)
     d["len"] = lens
     d["in_off"][1:] = np.cumsum(lens[:-1])  # 64-byte packing: both phases occur
+    d["out_off"][1:] = np.cumsum(lens[:-1] + np.uint64(40))  # 8-byte packed bodies: both classes occur
     plan = SegmentPlan(d, open_=False, seg_blocks=8)
     seg = plan.segments
     mlen = lens[seg["frame"]] + np.uint64(33)
     nb = seg["nblocks"].astype(np.int64)
     ph = ((d["in_off"][seg["frame"]] + np.uint64(64) * seg["first_block"].astype(np.uint64)) >> np.uint64(6)) & np.uint64(1)
-    key = 2 * nb + (1 - ph.astype(np.int64))
+    oc = ((d["out_off"][seg["frame"]] + np.uint64(64) * seg["first_block"].astype(np.uint64)) >> np.uint64(6)) & np.uint64(1)
+    key = 4 * nb + 2 * (1 - ph.astype(np.int64)) + (1 - oc.astype(np.int64))
     assert np.all(np.diff(key) <= 0)
+    assert len(set(oc.tolist())) == 2
     # every box block of every frame covered exactly once
     cover = {}
     for s in seg:

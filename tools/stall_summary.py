@@ -8,11 +8,14 @@ import statistics
 import sys
 
 root, cfg = sys.argv[1], sys.argv[2]
-KERNEL = {"4k": "k_seal_uniform", "100b": "k_seal_uniform", "open4k": "k_open_uniform", "zipf": "k_seal_segments_lines"}[cfg]
+sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
+from pmc_key import file_safe, parse  # noqa: E402
+KERNEL = {"4k": "k_seal_uniform", "4k_dense": "k_seal_uniform", "100b": "k_seal_uniform", "open4k": "k_open_uniform",
+          "zipf": "k_seal_segments_lines"}[parse(cfg)[0]]
 vals = collections.defaultdict(list)
 for p in (1, 2):
     rows = collections.defaultdict(dict)
-    for f in glob.glob(os.path.join(root, f"stall_{cfg}_{p}", "**", "*counter_collection.csv"), recursive=True):
+    for f in glob.glob(os.path.join(root, f"stall_{file_safe(cfg)}_{p}", "**", "*counter_collection.csv"), recursive=True):
         for r in csv.DictReader(open(f)):
             if KERNEL in r["Kernel_Name"]:
                 rows[int(r["Dispatch_Id"])][r["Counter_Name"]] = float(r["Counter_Value"])

@@ -12,9 +12,12 @@ import statistics
 import sys
 
 root, cfgs = sys.argv[1], sys.argv[2:]
+sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
+from pmc_key import file_safe, parse  # noqa: E402
 # the kernels that make up one timed launch of each config (setup kernels excluded)
 KERNELS = {"4k": ("k_seal_uniform",), "100b": ("k_seal_uniform",), "open4k": ("k_open_uniform",),
-           "zipf": ("k_seal_segments", "k_seal_combine"), "zipf_lane": ("k_seal_desc",)}
+           "zipf": ("k_seal_segments", "k_seal_combine"), "zipf_lane": ("k_seal_desc",),
+           "4k_dense": ("k_seal_uniform",)}
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 path = os.path.join(ROOT, "profiles", "pmc_traffic.json")
 data = json.load(open(path)) if os.path.exists(path) else {}
@@ -22,7 +25,7 @@ data = json.load(open(path)) if os.path.exists(path) else {}
 
 def per_kernel(pmc, cfg):
     vals = collections.defaultdict(list)
-    for f in glob.glob(os.path.join(root, f"traffic_{cfg}_{pmc}", "**", "*counter_collection.csv"), recursive=True):
+    for f in glob.glob(os.path.join(root, f"traffic_{file_safe(cfg)}_{pmc}", "**", "*counter_collection.csv"), recursive=True):
         for r in csv.DictReader(open(f)):
             name = r["Kernel_Name"].split("(")[-2].split("::")[-1] if "(" in r["Kernel_Name"] else r["Kernel_Name"]
             vals[name].append(float(r["Counter_Value"]))
@@ -30,7 +33,7 @@ def per_kernel(pmc, cfg):
 
 
 for cfg in cfgs:
-    keep = KERNELS.get(cfg, ("k_",))
+    keep = KERNELS.get(parse(cfg)[0], ("k_",))
     fetch = {k: v for k, v in per_kernel("FETCH_SIZE", cfg).items() if k.startswith(keep)}
     write = {k: v for k, v in per_kernel("WRITE_SIZE", cfg).items() if k.startswith(keep)}
     if not fetch or not write:

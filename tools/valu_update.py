@@ -14,8 +14,11 @@ import statistics
 import sys
 
 root, cfgs = sys.argv[1], sys.argv[2:]
+sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
+from pmc_key import file_safe, parse  # noqa: E402
 KERNELS = {"4k": ("k_seal_uniform",), "100b": ("k_seal_uniform",), "open4k": ("k_open_uniform",),
-           "zipf": ("k_seal_segments", "k_seal_combine"), "zipf_lane": ("k_seal_desc",)}
+           "zipf": ("k_seal_segments", "k_seal_combine"), "zipf_lane": ("k_seal_desc",),
+           "4k_dense": ("k_seal_uniform",)}
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 path = os.path.join(ROOT, "profiles", "pmc_traffic.json")
 data = json.load(open(path)) if os.path.exists(path) else {}
@@ -26,10 +29,10 @@ def short(n):
 
 
 for cfg in cfgs:
-    keep = KERNELS.get(cfg, ("k_",))
+    keep = KERNELS.get(parse(cfg)[0], ("k_",))
     vals = collections.defaultdict(lambda: collections.defaultdict(list))
     dur = collections.defaultdict(list)
-    for f in glob.glob(os.path.join(root, f"valu_{cfg}", "**", "*counter_collection.csv"), recursive=True):
+    for f in glob.glob(os.path.join(root, f"valu_{file_safe(cfg)}", "**", "*counter_collection.csv"), recursive=True):
         for r in csv.DictReader(open(f)):
             k = short(r["Kernel_Name"])
             if not k.startswith(keep):

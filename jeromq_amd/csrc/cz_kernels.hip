@@ -2508,21 +2508,26 @@ __global__ __launch_bounds__(BLOCK) void k_fill(uint8_t *__restrict__ buf, uint6
     }
 }
 
-// Device-to-device copy, 16-byte loads and stores, 4 in flight per thread (bench.py's HBM copy
-// ceiling: the float4 copy of the MI355X guide)
+// Device-to-device copy (bench.py's HBM copy ceiling, the guide's float4 copy): each workgroup
+// copies one contiguous 16 KiB tile, 4 x 16-byte loads in flight per thread, every wave
+// instruction 1 KiB contiguous.  tools/diag/copy_ub.hip on MI355X: this form 5.6 TB/s (read +
+// write), grid-stride loops 4.4-4.7, hipMemcpy D2D 4.9, torch copy_ 4.7-4.9.
 __global__ __launch_bounds__(BLOCK) void k_copy16(uint4 *__restrict__ dst, const uint4 *__restrict__ src, uint64_t n16)
 {
-    const uint64_t stride = (uint64_t)gridDim.x * BLOCK;
-    uint64_t i = (uint64_t)blockIdx.x * BLOCK + threadIdx.x;
-    for (; i + 3 * stride < n16; i += 4 * stride) {
-        const uint4 a = src[i], b = src[i + stride], c = src[i + 2 * stride], d = src[i + 3 * stride];
-        dst[i] = a;
-        dst[i + stride] = b;
-        dst[i + 2 * stride] = c;
-        dst[i + 3 * stride] = d;
+    const uint64_t base = (uint64_t)blockIdx.x * BLOCK * 4;
+    uint4 v[4];
+#pragma unroll
+    for (int u = 0; u < 4; u++) {
+        const uint64_t i = base + u * BLOCK + threadIdx.x;
+        if (i < n16)
+            v[u] = src[i];
     }
-    for (; i < n16; i += stride)
-        dst[i] = src[i];
+#pragma unroll
+    for (int u = 0; u < 4; u++) {
+        const uint64_t i = base + u * BLOCK + threadIdx.x;
+        if (i < n16)
+            dst[i] = v[u];
+    }
 }
 
 // Staging choice for a uniform batch (all pointers 16-byte aligned assumed by the caller check).
@@ -2739,9 +2744,10 @@ hipError_t czk_copy16(void *dst, const void *src, uint64_t nbytes, hipStream_t s
     const uint64_t n16 = nbytes / 16;
     if (n16 == 0)
         return hipSuccess;
-    const uint64_t want = (n16 + 4 * BLOCK - 1) / (4 * BLOCK);
-    const unsigned blocks = (unsigned)(want < 256 * 16 ? want : 256 * 16);  // 16 workgroups per CU
-    hipLaunchKernelGGL(k_copy16, dim3(blocks), dim3(BLOCK), 0, s, (uint4 *)dst, (const uint4 *)src, n16);
+    const uint64_t blocks = (n16 + 4 * BLOCK - 1) / (4 * BLOCK);
+    if (blocks > 0x7fffffffull)
+        return hipErrorInvalidValue;
+    hipLaunchKernelGGL(k_copy16, dim3((unsigned)blocks), dim3(BLOCK), 0, s, (uint4 *)dst, (const uint4 *)src, n16);
     return hipGetLastError();
 }
 

@@ -40,6 +40,26 @@ SINGLE = {
     "v_pk_mov_b32": "v_pk_mov_b32 v[{a}:{b}], v[4:5], v[{a}:{b}] op_sel:[0,1]",
     "v_bfe_u32": "v_bfe_u32 v{n}, v{n}, 3, 20",
     "v_min3_u32": "v_min3_u32 v{n}, v{n}, v4, v5",
+    # left-shift candidates (v_lshlrev_b32 issues in 4 cycles, v_lshrrev_b32 in 2)
+    "v_lshlrev_b32 vgpr amt": "v_lshlrev_b32_e32 v{n}, v6, v{n}",
+    "v_lshrrev_b32 vgpr amt": "v_lshrrev_b32_e32 v{n}, v6, v{n}",
+    "v_ashrrev_i32_e32": "v_ashrrev_i32_e32 v{n}, 7, v{n}",
+    "v_lshlrev_b16_e32": "v_lshlrev_b16_e32 v{n}, 7, v{n}",
+    "v_lshrrev_b16_e32": "v_lshrrev_b16_e32 v{n}, 7, v{n}",
+    "v_add_u16_e32": "v_add_u16_e32 v{n}, v4, v{n}",
+    "v_mul_lo_u16_e32": "v_mul_lo_u16_e32 v{n}, v4, v{n}",
+    "v_bfrev_b32": "v_bfrev_b32_e32 v{n}, v{n}",
+    "v_subrev_u32_e32": "v_subrev_u32_e32 v{n}, v4, v{n}",
+    "v_add_u32 sdwa w1": "v_add_u32_sdwa v{n}, v{n}, v{n} dst_sel:WORD_1 dst_unused:UNUSED_PAD src0_sel:DWORD src1_sel:DWORD",
+    "v_xor_b32 sdwa": "v_xor_b32_sdwa v{n}, v{n}, v4 dst_sel:DWORD dst_unused:UNUSED_PAD src0_sel:WORD_1 src1_sel:DWORD",
+    "v_lshlrev_b32 sdwa": "v_lshlrev_b32_sdwa v{n}, v6, v{n} dst_sel:DWORD dst_unused:UNUSED_PAD src0_sel:DWORD src1_sel:DWORD",
+    "v_xor_b32 dpp": "v_xor_b32_dpp v{n}, v{n}, v4 quad_perm:[1,0,3,2] row_mask:0xf bank_mask:0xf",
+    "v_mul_f32 imm": "v_mul_f32_e32 v{n}, 0x43000000, v{n}",
+    "v_ldexp_f32": "v_ldexp_f32 v{n}, v{n}, 7",
+    "v_cndmask_b32 sgpr": "v_cndmask_b32_e64 v{n}, v4, v{n}, s[0:1]",
+    "v_max_f32": "v_max_f32_e32 v{n}, v4, v{n}",
+    "v_med3_f32": "v_med3_f32 v{n}, v{n}, v4, v5",
+    "v_exp_f32": "v_exp_f32_e32 v{n}, v{n}",
 }
 PAIRED = {"v_fma_f64", "v_lshrrev_b64", "v_pk_mov_b32"}
 
@@ -52,6 +72,8 @@ MIX = {  # pattern of F / S over 16 instructions
     "mix F8S8": "F" * 8 + "S" * 8,
     "mix F2S1": "FFSFFSFFSFFSFFSF",
     "mix F3S1": "FFFS" * 4,
+    "mix F15S1": "F" * 15 + "S",
+    "mix F7S1": "FFFFFFFS" * 2,
 }
 
 

@@ -21,7 +21,7 @@ using namespace cz;
 
 #define UB_CLOB                                                                                                    \
     "v8", "v9", "v10", "v11", "v12", "v13", "v14", "v15", "v16", "v17", "v18", "v19", "v20", "v21", "v22", "v23", \
-        "v24", "v25", "v26", "v27", "v28", "v29", "v30", "v31", "vcc", "s2"
+        "v24", "v25", "v26", "v27", "v28", "v29", "v30", "v31", "vcc", "s0", "s1", "s2"
 #include "issue_ub2.inc"
 
 #define CK(x)                                                                  \
@@ -38,7 +38,7 @@ enum { K_SALSA_ALIGN = 1000, K_SALSA_SHIFT = 1001, K_SALSA_LAZY = 1002, K_SALSA_
 __device__ __forceinline__ void ub_init()
 {
     asm volatile("v_mov_b32 v4, 0x3f800001\n v_mov_b32 v5, 0x3f7ffffe\n v_mov_b32 v6, 0x3f800003\n"
-                 "v_mov_b32 v7, 0x3f000001\n s_mov_b32 s2, 0x9e3779b9\n s_mov_b64 vcc, 0\n"
+                 "v_mov_b32 v7, 0x3f000001\n s_mov_b32 s2, 0x9e3779b9\n s_mov_b64 vcc, 0\n s_mov_b64 s[0:1], 0\n"
                  "v_mov_b32 v8, v4\n v_mov_b32 v9, v5\n v_mov_b32 v10, v6\n v_mov_b32 v11, v7\n"
                  "v_mov_b32 v12, v4\n v_mov_b32 v13, v5\n v_mov_b32 v14, v6\n v_mov_b32 v15, v7\n"
                  "v_mov_b32 v16, v4\n v_mov_b32 v17, v5\n v_mov_b32 v18, v6\n v_mov_b32 v19, v7\n"

@@ -19,3 +19,6 @@ echo "== latency floors"
 timeout -k 10 120 ./tools/diag/latency_ub > gpurun_out/r03/latency_ub2.log 2>&1 || { tail gpurun_out/r03/latency_ub2.log; exit 3; }
 timeout -k 10 120 ./tools/diag/latency_ub spin >> gpurun_out/r03/latency_ub2.log 2>&1 || { tail gpurun_out/r03/latency_ub2.log; exit 3; }
 cat gpurun_out/r03/latency_ub2.log
+echo "== issue probe (left-shift candidates)"
+timeout -k 10 400 ./tools/diag/issue_ub2 256 > gpurun_out/r03/issue_ub3.log 2>&1 || { tail gpurun_out/r03/issue_ub3.log; exit 3; }
+grep -E "lshl|lshr|ashr|b16|u16|bfrev|subrev|sdwa|dpp|imm|ldexp|cndmask|max_f32|med3|exp_f32|F15S1|F7S1" gpurun_out/r03/issue_ub3.log

@@ -55,8 +55,8 @@ def parse():
                     help="4k/100b/open4k: body slot stride in bytes (0 = the config's own layout)")
     ap.add_argument("--plain-stride", type=int, default=0,
                     help="open4k: plaintext slot stride in bytes (0 = the payload stride, 4096)")
-    ap.add_argument("--config", default="4k", choices=["4k", "4k_dense", "100b", "zipf", "zipf_lane", "open4k", "e2e4k", "engine", "nacl",
-                                                          "beforenm"])
+    ap.add_argument("--config", default="4k", choices=["4k", "4k_dense", "4k_box", "100b", "zipf", "zipf_lane", "open4k", "e2e4k",
+                                                          "engine", "nacl", "beforenm"])
     ap.add_argument("--frames", type=int, default=FRAMES)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-scatter", action="store_true",
@@ -121,7 +121,7 @@ def shard_plan(rank, frames_per_rank, cfg="4k"):
     """Rank r seals frames [r*F, (r+1)*F) of the global batch: nonce counters 3 + r*F ..,
     its own payload seed.  Frames are independent, so no data crosses ranks (weak scaling)."""
     counter0 = 3 + rank * frames_per_rank
-    seed = 0x5EED0000 + {"4k": 1, "4k_dense": 1, "100b": 2, "zipf": 3, "zipf_lane": 3, "open4k": 4}[cfg] + 1000 * rank
+    seed = 0x5EED0000 + {"4k": 1, "4k_dense": 1, "4k_box": 1, "100b": 2, "zipf": 3, "zipf_lane": 3, "open4k": 4}[cfg] + 1000 * rank
     return counter0, seed
 
 
@@ -136,7 +136,23 @@ class Workload:
         self.subkey = batch.subkeys(key, _lib.CZ_DIR_C2S)[0].contiguous()
         self.counter0, seed = shard_plan(rank, frames, cfg)
         self.count = frames
-        if cfg in ("4k", "4k_dense", "100b", "open4k"):
+        if cfg == "4k_box":
+            # the reference's own box layout as input (CurveClientMechanism.java:144-153): slot i =
+            # 0^32 || flags || payload, 4224-byte slots in and out
+            n = 4096
+            self.n = n
+            self.in_stride = self.out_stride = 4224
+            self.d_in = torch.empty(frames * self.in_stride, dtype=torch.uint8, device=dev)
+            batch.fill(self.d_in, seed)
+            box = self.d_in.view(frames, self.in_stride)
+            box[:, :32] = 0
+            box[:, 32] = 0
+            box[::8, 32] = 1
+            self.d_out = torch.empty(frames * self.out_stride, dtype=torch.uint8, device=dev)
+            self.payload_bytes = frames * n
+            self.read_bytes = frames * (n + 1)   # flags byte + payload (box bytes 0..31 are not read)
+            self.write_bytes = frames * (n + 33)
+        elif cfg in ("4k", "4k_dense", "100b", "open4k"):
             n = 4096 if cfg != "100b" else 100
             self.n = n
             self.in_stride = (n + 15) // 16 * 16
@@ -214,7 +230,10 @@ class Workload:
         torch.cuda.synchronize()
 
     def step(self):
-        if self.cfg in ("4k", "4k_dense", "100b"):
+        if self.cfg == "4k_box":
+            batch.seal_uniform_box(self.d_in, self.in_stride, self.d_out, self.out_stride, self.count, self.n,
+                                   self.subkey, self.counter0)
+        elif self.cfg in ("4k", "4k_dense", "100b"):
             batch.seal_uniform(self.d_in, self.in_stride, self.d_out, self.out_stride, self.count, self.n,
                                self.subkey, self.counter0, flags8=self.flags)
         elif self.cfg == "open4k":
@@ -231,9 +250,10 @@ class Workload:
         sys.path.insert(0, os.path.join(ROOT, "tests"))
         from cz_testlib import or_curve_encode
         torch.cuda.synchronize()
-        if self.cfg in ("4k", "4k_dense", "100b"):
+        if self.cfg in ("4k", "4k_dense", "100b", "4k_box"):
+            skip = 33 if self.cfg == "4k_box" else 0
             for i in (0, 1, 7, self.count // 2, self.count - 2, self.count - 1):
-                p = self.d_in[i * self.in_stride:i * self.in_stride + self.n].cpu().numpy().tobytes()
+                p = self.d_in[i * self.in_stride + skip:i * self.in_stride + skip + self.n].cpu().numpy().tobytes()
                 body = self.d_out[i * self.out_stride:i * self.out_stride + self.n + 33].cpu().numpy().tobytes()
                 fl = 1 if i % 8 == 0 else 0
                 if body != or_curve_encode(p, fl, self.counter0 + i, 0, PRECOM):
@@ -821,6 +841,8 @@ def main():
     if rank == 0:
         names = {"4k": "1M x 4 KiB frames, seal (configs[1])",
                  "4k_dense": "1M x 4 KiB frames, seal, bodies packed back to back (4129-byte slots)",
+                 "4k_box": "1M x 4 KiB frames, seal, input in the reference's box layout (0^32 || flags || payload, "
+                           "4224-byte slots)",
                  "100b": "1M x 100 B frames, seal (configs[2])",
                  "zipf": "1M Zipf(1.2) 64 B..64 KiB frames, seal, segmented (configs[3])",
                  "zipf_lane": "1M Zipf(1.2) 64 B..64 KiB frames, seal, lane per frame (configs[3])",

@@ -99,10 +99,17 @@ typedef struct cz_frame_desc {
  * Replaces curve25519xsalsa20poly1305.crypto_box_afternm (called at Curve.java:136)
  * and crypto_box_open_afternm (Curve.java:146); crypto_secretbox[_open]
  * (xsalsa20poly1305, Curve.java:166,176) is the same primitive.
- * m[0:32] must be zero; c[0:16] is written as zero.  Runs on the GPU (one
- * launch per call: latency-bound -- use the batched API for throughput). */
+ * m[0:32] must be zero (NaCl's ZEROBYTES contract; a seal returns -1 otherwise rather than
+ * produce different bytes); c[0:16] is written as zero.  Runs on the GPU in one launch per call
+ * (boxes up to 80 KiB; larger ones through the segmented kernels): latency-bound, ~11 us of
+ * launch + sync floor -- use the batched API for throughput. */
 int cz_box_afternm(uint8_t *c, const uint8_t *m, uint64_t mlen, const uint8_t n[24], const uint8_t k[32]);
 int cz_box_open_afternm(uint8_t *m, const uint8_t *c, uint64_t clen, const uint8_t n[24], const uint8_t k[32]);
+/* The one-launch drop-ins above keep, per calling thread, the HSalsa20 subkeys of the last 8
+ * (k, n[0:16]) pairs in device memory (CurveZMQ: one pair per connection direction), so repeated
+ * calls on a connection skip the derivation.  Wipe this thread's cache (host copy of the keys and
+ * the device subkeys). */
+int cz_nacl_forget(void);
 int cz_secretbox(uint8_t *c, const uint8_t *m, uint64_t mlen, const uint8_t n[24], const uint8_t k[32]);
 int cz_secretbox_open(uint8_t *m, const uint8_t *c, uint64_t clen, const uint8_t n[24], const uint8_t k[32]);
 
@@ -134,6 +141,13 @@ int cz_open_batch(const cz_frame_desc *d_desc, const uint32_t *d_order, uint32_t
 int cz_seal_uniform(uint32_t count, uint32_t len, const void *d_in, uint64_t in_stride, void *d_out,
                     uint64_t out_stride, const void *d_subkey, uint64_t counter0, const uint8_t *d_flags8,
                     void *stream);
+/* The same batch from input already in the reference's NaCl box layout: slot i holds the box
+ * m = 0^32 || flags || payload (len = payload bytes, so a box is len + 33 bytes), exactly the
+ * buffer CurveClientMechanism.encode builds and hands to Curve.afternm (CurveClientMechanism.java:
+ * 144-153, Curve.java:134-137).  The flags byte comes from box byte 32; box bytes 0..31 are not
+ * read.  Output as cz_seal_uniform.  Input read where it lies: no byte shift on the device. */
+int cz_seal_uniform_box(uint32_t count, uint32_t len, const void *d_box, uint64_t box_stride, void *d_out,
+                        uint64_t out_stride, const void *d_subkey, uint64_t counter0, void *stream);
 /* Open `count` bodies of `size` bytes of one connection in order; frame 0 must
  * beat floor0, frame i must beat frame i-1 (when check != 0).  Payload i goes to
  * out + i*out_stride; the batch owns count * out_stride output bytes (slot bytes

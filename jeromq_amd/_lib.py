@@ -98,6 +98,7 @@ SIGNATURES = {
     "cz_seal_batch": (_I, [_VP, _VP, _U32, _VP, _VP, _VP, _VP]),
     "cz_open_batch": (_I, [_VP, _VP, _U32, _VP, _VP, _VP, _VP, _VP, _VP]),
     "cz_seal_uniform": (_I, [_U32, _U32, _VP, _U64, _VP, _U64, _VP, _U64, _VP, _VP]),
+    "cz_seal_uniform_box": (_I, [_U32, _U32, _VP, _U64, _VP, _U64, _VP, _U64, _VP]),
     "cz_open_uniform": (_I, [_U32, _U32, _VP, _U64, _VP, _U64, _VP, _U64, _I, _VP, _VP]),
     "cz_plan_order": (_I, [_VP, _U32, _VP]),
     "cz_plan_segments": (_I, [_VP, _U32, _I, _U32, _VP, _U32, ctypes.POINTER(_U32), _VP, _U32,
@@ -106,6 +107,7 @@ SIGNATURES = {
     "cz_open_segments": (_I, [_VP, _VP, _U32, _VP, _U32, _VP, _VP, _VP, _VP, _VP, _VP, _VP]),
     "cz_fill": (_I, [_VP, _U64, _U64, _VP]),
     "cz_dev_copy": (_I, [_VP, _VP, _U64, _VP]),
+    "cz_nacl_forget": (_I, []),
     "cz_ctx_create": (_I, [ctypes.POINTER(_VP), _I]),
     "cz_ctx_destroy": (None, [_VP]),
     "cz_ctx_set_keys": (_I, [_VP, _VP, _U32, _I]),

@@ -58,6 +58,18 @@ def seal_uniform(inp, in_stride, out, out_stride, count, length, subkey, counter
                                           counter0, _ptr(flags8), _stream(stream)), "cz_seal_uniform")
 
 
+def seal_uniform_box(box, box_stride, out, out_stride, count, length, subkey, counter0, stream=None):
+    """Uniform seal from the reference's box layout: slot i of `box` holds 0^32 || flags ||
+    payload (length = payload bytes), as CurveClientMechanism.encode hands it to Curve.afternm."""
+    _need_cuda_u8(box, "box")
+    _need_cuda_u8(out, "out")
+    if count:  # (like seal_uniform, the batch owns whole output slots)
+        if box.numel() < (count - 1) * box_stride + length + 33 or out.numel() < count * out_stride:
+            raise ValueError("seal_uniform_box: buffers smaller than the batch")
+    _lib.check(_lib.lib().cz_seal_uniform_box(count, length, _ptr(box), box_stride, _ptr(out), out_stride,
+                                              _ptr(subkey), counter0, _stream(stream)), "cz_seal_uniform_box")
+
+
 def open_uniform(inp, in_stride, out, out_stride, count, size, subkey, floor0, status, check=True, stream=None):
     """Open `count` bodies of `size` bytes of one connection, in order; payload i goes to
     slot out[i*out_stride : (i+1)*out_stride] (whole slots owned by the batch)."""

@@ -16,6 +16,8 @@
 #include "cz_internal.h"
 
 extern "C" {
+hipError_t czk_seal_uniform_box(const void *, uint64_t, void *, uint64_t, uint32_t, uint32_t, const void *, uint64_t,
+                                hipStream_t);
 hipError_t czk_seal_uniform(const void *, uint64_t, void *, uint64_t, uint32_t, uint32_t, const void *, uint64_t,
                             const uint8_t *, hipStream_t);
 hipError_t czk_seal_desc(const cz_frame_desc *, const uint32_t *, uint32_t, const void *, void *, const void *,
@@ -25,6 +27,8 @@ hipError_t czk_open_desc(const cz_frame_desc *, const uint32_t *, uint32_t, cons
 hipError_t czk_open_uniform(const void *, uint64_t, void *, uint64_t, uint32_t, uint32_t, const void *, uint64_t, int,
                             uint16_t *, hipStream_t);
 hipError_t czk_box_nacl(const void *, void *, uint32_t, const void *, uint64_t, int, int *, hipStream_t);
+hipError_t czk_nacl_one(void *, uint32_t, int, void *, int, uint32_t, hipStream_t);
+uint32_t czk_nacl_one_max(void);
 hipError_t czk_fill(void *, uint64_t, uint64_t, hipStream_t);
 hipError_t czk_copy16(void *, const void *, uint64_t, hipStream_t);
 int czk_tune(const char *, int);
@@ -108,11 +112,28 @@ void HostBuf::release()
 // Salsa20 blocks on one lane (k_box_nacl keeps only mlen == 32, which has no MESSAGE form).
 // Everything the device needs -- key, descriptor, segment and combine lists, the message -- goes
 // over in ONE pinned H2D copy, and the result in one D2H copy.
+// One-launch path (k_nacl_one): the staging is pinned host memory the kernel reads and writes
+// directly, and the subkey HSalsa20(k, n[0:16]) of the last NCACHE (k, n[0:16]) pairs this thread
+// used stays in device memory (CurveZMQ: one pair per connection direction).  cz_nacl_forget()
+// wipes both.
 struct Single {
+    static constexpr int NCACHE = 8;
     bool ready = false;
     hipStream_t stream = nullptr;
-    DevBuf dev, rc;
-    HostBuf stage;
+    DevBuf dev, rc, subcache;
+    HostBuf stage, one;
+    uint8_t ckey[NCACHE][48] = {};  // k || n[0:16] of each cached subkey
+    bool cvalid[NCACHE] = {};
+    int cnext = 0;
+    ~Single() { forget_host(); }
+    void forget_host()
+    {
+        explicit_bzero(ckey, sizeof ckey);
+        for (bool &v : cvalid)
+            v = false;
+        if (one.ptr)
+            explicit_bzero(one.ptr, 64);
+    }
 };
 
 static thread_local Single t_single;
@@ -128,7 +149,7 @@ static int single_init()
     e = hipStreamCreateWithFlags(&t_single.stream, hipStreamNonBlocking);
     if (e != hipSuccess)
         return hip_fail(e, "hipStreamCreate");
-    if ((e = t_single.rc.reserve(64)) != hipSuccess)
+    if ((e = t_single.rc.reserve(64)) != hipSuccess || (e = t_single.subcache.reserve(32 * Single::NCACHE)) != hipSuccess)
         return hip_fail(e, "hipMalloc");
     t_single.ready = true;
     return CZ_OK;
@@ -147,6 +168,67 @@ static uint32_t single_seg_blocks(uint32_t nblk)
     return s;
 }
 
+// NaCl box/open of one message in ONE launch (k_nacl_one): input staged into pinned host memory
+// the kernel reads directly, output read back from it after the launch.  -1 on a bad tag (dst
+// untouched) or a seal whose m[0:32] is not zero (NaCl's crypto_box_afternm contract: the MAC key
+// is c[0:32] = keystream ^ m[0:32], which the device path keeps as the keystream alone).
+static int nacl_one_launch(uint8_t *dst, const uint8_t *src, uint64_t len, const uint8_t n[24], const uint8_t k[32],
+                           int open)
+{
+    Single &s = t_single;
+    const uint64_t out_off = 128 + ((len + 127) & ~127ull);
+    hipError_t e;
+    if ((e = s.one.reserve(out_off + len + 128)) != hipSuccess) {
+        hip_fail(e, "hipHostMalloc");
+        return -1;
+    }
+    uint8_t *st = (uint8_t *)s.one.ptr;
+    // subkey cache: (k, n[0:16]) -> device slot
+    int slot = -1;
+    for (int i = 0; i < Single::NCACHE; i++)
+        if (s.cvalid[i] && memcmp(s.ckey[i], k, 32) == 0 && memcmp(s.ckey[i] + 32, n, 16) == 0) {
+            slot = i;
+            break;
+        }
+    const int miss = slot < 0;
+    if (miss) {
+        slot = s.cnext;
+        s.cnext = (s.cnext + 1) % Single::NCACHE;
+        memcpy(s.ckey[slot], k, 32);
+        memcpy(s.ckey[slot] + 32, n, 16);
+        s.cvalid[slot] = false;  // valid once the launch that derives it has completed
+        memcpy(st, k, 32);
+    }
+    memcpy(st + 32, n, 24);
+    memcpy(st + 128, src, len);
+    *(volatile int *)(st + 56) = -2;
+    if ((e = czk_nacl_one(st, (uint32_t)len, open, (uint8_t *)s.subcache.ptr + 32 * slot, miss, (uint32_t)out_off,
+                          s.stream)) != hipSuccess ||
+        (e = hipStreamSynchronize(s.stream)) != hipSuccess) {
+        explicit_bzero(st, 32);
+        hip_fail(e, "cz_box (one launch)");
+        return -1;
+    }
+    if (miss) {
+        explicit_bzero(st, 32);
+        s.cvalid[slot] = true;
+    }
+    const int rc = *(volatile int *)(st + 56);
+    if (!open) {
+        memset(dst, 0, 16);
+        memcpy(dst + 16, st + out_off + 16, len - 16);
+        return rc == 0 ? 0 : -1;
+    }
+    if (rc != 0) {
+        explicit_bzero(st + out_off, len);  // never leave unauthenticated plaintext behind
+        return -1;
+    }
+    memset(dst, 0, 32);
+    memcpy(dst + 32, st + out_off + 32, len - 32);
+    explicit_bzero(st + out_off, len);
+    return 0;
+}
+
 // NaCl box/open of one message on the device.  A MESSAGE is the NaCl box of
 // 0^32 || flags || payload, so m[32] rides as the flags byte and m[33:] as the payload; for open
 // the 16 bytes ahead of the tag are rebuilt as "\x07MESSAGE" || n[16:24] and the nonce check is off.
@@ -157,8 +239,18 @@ static int nacl_one(uint8_t *dst, const uint8_t *src, uint64_t len, const uint8_
         return -1;
     if (len < 32 || len > 0xffffffffull)
         return -1;
+    if (!open) {  // crypto_box_afternm's contract: m starts with 32 zero bytes
+        uint8_t z = 0;
+        for (int i = 0; i < 32; i++)
+            z |= src[i];
+        if (z)
+            return fail(CZ_EINVAL, "cz_box_afternm: m[0:32] is not zero (NaCl ZEROBYTES)"), -1;
+    }
     if (single_init() != CZ_OK)
         return -1;
+    static const bool segmented_only = getenv("CZ_NACL_SEGMENTED") != nullptr;  // A/B: the multi-launch path
+    if (len <= czk_nacl_one_max() && !segmented_only)
+        return nacl_one_launch(dst, src, len, n, k, open);
     Single &s = t_single;
     uint64_t counter = 0;
     for (int i = 0; i < 8; i++)
@@ -396,6 +488,20 @@ int cz_box_afternm(uint8_t *c, const uint8_t *m, uint64_t mlen, const uint8_t n[
     return nacl_one(c, m, mlen, n, k, 0);
 }
 
+int cz_nacl_forget(void)
+{
+    Single &s = t_single;
+    s.forget_host();
+    if (s.ready && s.subcache.ptr) {
+        hipError_t e = hipMemsetAsync(s.subcache.ptr, 0, s.subcache.cap, s.stream);
+        if (e == hipSuccess)
+            e = hipStreamSynchronize(s.stream);
+        if (e != hipSuccess)
+            return hip_fail(e, "cz_nacl_forget");
+    }
+    return CZ_OK;
+}
+
 int cz_box_open_afternm(uint8_t *m, const uint8_t *c, uint64_t clen, const uint8_t n[24], const uint8_t k[32])
 {
     return nacl_one(m, c, clen, n, k, 1);
@@ -479,6 +585,20 @@ int cz_seal_uniform(uint32_t count, uint32_t len, const void *d_in, uint64_t in_
     hipError_t e = czk_seal_uniform(d_in, in_stride, d_out, out_stride, count, len, d_subkey, counter0, d_flags8,
                                     (hipStream_t)stream);
     return e == hipSuccess ? CZ_OK : hip_fail(e, "cz_seal_uniform");
+}
+
+int cz_seal_uniform_box(uint32_t count, uint32_t len, const void *d_box, uint64_t box_stride, void *d_out,
+                        uint64_t out_stride, const void *d_subkey, uint64_t counter0, void *stream)
+{
+    if (count && (!d_box || !d_out || !d_subkey))
+        return fail(CZ_EINVAL, "cz_seal_uniform_box: null pointer");
+    if ((uint64_t)len + CZ_MESSAGE_OVERHEAD > 0xffffffffull)
+        return fail(CZ_EINVAL, "cz_seal_uniform_box: frame too large");
+    if (count > 1 && (box_stride < (uint64_t)len + CZ_MESSAGE_OVERHEAD || out_stride < (uint64_t)len + CZ_MESSAGE_OVERHEAD))
+        return fail(CZ_EINVAL, "cz_seal_uniform_box: stride smaller than the frame");
+    hipError_t e = czk_seal_uniform_box(d_box, box_stride, d_out, out_stride, count, len, d_subkey, counter0,
+                                        (hipStream_t)stream);
+    return e == hipSuccess ? CZ_OK : hip_fail(e, "cz_seal_uniform_box");
 }
 
 int cz_open_uniform(uint32_t count, uint32_t size, const void *d_in, uint64_t in_stride, void *d_out,

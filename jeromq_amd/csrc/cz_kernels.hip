@@ -46,7 +46,10 @@ using namespace cz;
 
 namespace {
 
-enum Mode { MODE_ZMQ = 0, MODE_NACL = 1 };
+// MODE_BOX: MESSAGE output (as MODE_ZMQ) from input already in the reference's box layout,
+// m = 0^32 || flags || payload (CurveClientMechanism.java:144-153 builds exactly this and hands it
+// to Curve.afternm): box blocks are read where they lie, no funnel shift, no carried words.
+enum Mode { MODE_ZMQ = 0, MODE_NACL = 1, MODE_BOX = 2 };
 
 // "\x07MESSAGE" as two little-endian words
 constexpr u32 HDR0 = 0x53454d07u, HDR1 = 0x45474153u;
@@ -548,10 +551,12 @@ __device__ __forceinline__ void seal_frame(const uint8_t *__restrict__ in, u32 n
     // ZMQ funnel: box dword k of block b = alignbyte(P[16b+k-8], P[16b+k-9], 3)
     // where P[i] is payload dword i; block b's window is P[16b-8 .. 16b+7]
     // (payload bytes [64b-32, 64b+32)) and P[16b-9] is carried from block b-1.
-    const u32 mlen = (MODE == MODE_ZMQ) ? n + 33u : n;
+    // MODE_BOX: n = payload bytes, `in` = the box (mlen bytes; box bytes 0..31 are not read, the
+    // flags byte is box byte 32 and `flags` is ignored)
+    const u32 mlen = (MODE == MODE_ZMQ || MODE == MODE_BOX) ? n + 33u : n;
     const u32 nfull = mlen >> 6;
     const u32 tailv = mlen & 63u;
-    const u64 inlen = n;
+    const u64 inlen = MODE == MODE_BOX ? (u64)mlen : (u64)n;
     u32 n0, n1;
     counter_nonce(counter, n0, n1);
     if constexpr (UN0)
@@ -585,9 +590,68 @@ __device__ __forceinline__ void seal_frame(const uint8_t *__restrict__ in, u32 n
         em.emit_full(blk, C);
     };
 
-    u32 carry;
+    // box-aligned input, one full block b >= 1 from its 16 dwords
+    [[maybe_unused]] auto box_full_block = [&](u32 blk, const u32 *W) {
+        ksblock(x, blk, 0u);
+#pragma unroll
+        for (int k = 0; k < 16; k++)
+            C[k] = W[k] ^ x[k];
+        poly_block(P, C[0], C[1], C[2], C[3], 1u);
+        poly_block(P, C[4], C[5], C[6], C[7], 1u);
+        poly_block(P, C[8], C[9], C[10], C[11], 1u);
+        poly_block(P, C[12], C[13], C[14], C[15], 1u);
+        em.emit_full(blk, C);
+    };
+
+    u32 carry = 0;
     u32 blk = 1;
-    if constexpr (MODE == MODE_ZMQ && AL && PAIR) {
+    if constexpr (MODE == MODE_BOX && AL && PAIR) {
+        // Whole-line input straight from the box: line k = box blocks 2k and 2k+1 (line 0: bytes
+        // 32..63 of block 0 and block 1), 8 back-to-back loads per line, nothing carried.
+        u32 L[32];
+#pragma unroll
+        for (int c = 2; c < 8; c++) {
+            V4 v = ld16<AL>(in + 16 * c, inlen > 16u * c ? inlen - 16u * c : 0);
+            L[4 * c] = v.x; L[4 * c + 1] = v.y; L[4 * c + 2] = v.z; L[4 * c + 3] = v.w;
+        }
+#pragma unroll
+        for (int k = 8; k < 16; k++)
+            C[k] = L[k] ^ x[k];
+        C[0] = HDR0; C[1] = HDR1; C[2] = n0; C[3] = n1;
+        C[4] = C[5] = C[6] = C[7] = 0u;
+        if (nfull >= 1) {
+            poly_block(P, C[8], C[9], C[10], C[11], 1u);
+            poly_block(P, C[12], C[13], C[14], C[15], 1u);
+        } else {
+            const u32 nb = mlen - 32u;
+            if (nb >= 16u) {
+                poly_block(P, C[8], C[9], C[10], C[11], 1u);
+                if (nb > 16u)
+                    poly_block_partial(P, C[12], C[13], C[14], C[15], nb - 16u);
+            } else {
+                poly_block_partial(P, C[8], C[9], C[10], C[11], nb);
+            }
+        }
+        em.emit(0, C);
+        if (nfull >= 2) {
+            box_full_block(1, L + 16);
+            for (u32 k = 1; 2u * k + 1u < nfull; k++) {
+                const uint8_t *src = in + 128u * k;
+#pragma unroll
+                for (int c = 0; c < 8; c++) {
+                    V4 v = ld16f<AL>(src + 16 * c);
+                    L[4 * c] = v.x; L[4 * c + 1] = v.y; L[4 * c + 2] = v.z; L[4 * c + 3] = v.w;
+                }
+                box_full_block(2u * k, L);
+                box_full_block(2u * k + 1u, L + 16);
+                blk = 2u * k + 2u;
+            }
+            if (blk < 2u)
+                blk = 2u;
+        } else {
+            blk = nfull > 1 ? nfull : 1u;
+        }
+    } else if constexpr (MODE == MODE_ZMQ && AL && PAIR) {
         // Whole-line input: each lane reads payload line k = [128k, 128k+128) with
         // 8 back-to-back loads and uses it for blocks 2k and 2k+1 (block 2k's
         // window starts 36 bytes into line k-1: a 9-dword carry), so both halves
@@ -686,7 +750,11 @@ __device__ __forceinline__ void seal_frame(const uint8_t *__restrict__ in, u32 n
             C[8] = a.x ^ x[8]; C[9] = a.y ^ x[9]; C[10] = a.z ^ x[10]; C[11] = a.w ^ x[11];
             C[12] = b.x ^ x[12]; C[13] = b.y ^ x[13]; C[14] = b.z ^ x[14]; C[15] = b.w ^ x[15];
             carry = 0;
-            C[0] = C[1] = C[2] = C[3] = 0u;
+            if constexpr (MODE == MODE_BOX) {
+                C[0] = HDR0; C[1] = HDR1; C[2] = n0; C[3] = n1;
+            } else {
+                C[0] = C[1] = C[2] = C[3] = 0u;
+            }
         }
         C[4] = C[5] = C[6] = C[7] = 0u;  // tag slot, written by em.tag()
         if (nfull >= 1) {
@@ -858,11 +926,31 @@ __device__ __forceinline__ u32 open_frame(const uint8_t *__restrict__ in, u32 si
             em.emit(q, D);
     };
 
+    // Whole-line input: body line 0 -- tag, block 0 and block 1 -- leaves L2 in ONE burst, before
+    // block 0's keystream.  Read as before (block 1's half after block 0, ~6 us later under load)
+    // the line was often evicted in between and fetched twice: open FETCH was 1.075x its slot
+    // bytes against 1.03x for the seal, whose pair loop already reads whole lines.
+    constexpr bool EARLY0 = PAIR && AL && MODE == MODE_ZMQ;
+    const bool early0 = EARLY0 && nfull >= 2;
+    [[maybe_unused]] V4 e_tin{}, e_a{}, e_b{};
+    [[maybe_unused]] u32 L1[16];
+    if constexpr (EARLY0) {
+        if (early0) {
+            e_tin = ld16f<AL>(in + 16);
+            e_a = ld16f<AL>(in + 32);
+            e_b = ld16f<AL>(in + 48);
+#pragma unroll
+            for (int c = 0; c < 4; c++) {
+                V4 v = ld16f<AL>(in + 64 + 16 * c);
+                L1[4 * c] = v.x; L1[4 * c + 1] = v.y; L1[4 * c + 2] = v.z; L1[4 * c + 3] = v.w;
+            }
+        }
+    }
     u32 x[16], C[16], X[16];
     ksblock(x, 0u, 0u);
     Poly P;
     poly_init(P, x[0], x[1], x[2], x[3], x[4], x[5], x[6], x[7]);
-    V4 tin = ld16<AL>(in + 16, size - 16u);
+    V4 tin = early0 ? e_tin : ld16<AL>(in + 16, size - 16u);
 
     // ZMQ: payload chunk m (bytes [64m, 64m+64)) = box [64m+33, 64m+97): dword t is
     // alignbyte(D[16m+t+9], D[16m+t+8], 1), D = plaintext box dwords.  It is emitted
@@ -871,8 +959,8 @@ __device__ __forceinline__ u32 open_frame(const uint8_t *__restrict__ in, u32 si
 
     // block 0
     {
-        V4 a = ld16<AL>(in + 32, size > 32 ? size - 32u : 0);
-        V4 b = ld16<AL>(in + 48, size > 48 ? size - 48u : 0);
+        V4 a = early0 ? e_a : ld16<AL>(in + 32, size > 32 ? size - 32u : 0);
+        V4 b = early0 ? e_b : ld16<AL>(in + 48, size > 48 ? size - 48u : 0);
         C[8] = a.x; C[9] = a.y; C[10] = a.z; C[11] = a.w;
         C[12] = b.x; C[13] = b.y; C[14] = b.z; C[15] = b.w;
         if (nfull >= 1) {
@@ -954,15 +1042,9 @@ __device__ __forceinline__ u32 open_frame(const uint8_t *__restrict__ in, u32 si
     if constexpr (PAIR && AL) {
         // whole-line input: blocks 2k, 2k+1 come from one 8-load burst of body line k
         if (nfull >= 2) {
-            u32 L[16];
-#pragma unroll
-            for (int c = 0; c < 4; c++) {
-                V4 v = ld16f<AL>(in + 64 + 16 * c);
-                L[4 * c] = v.x; L[4 * c + 1] = v.y; L[4 * c + 2] = v.z; L[4 * c + 3] = v.w;
-            }
 #pragma unroll
             for (int k = 0; k < 16; k++)
-                C[k] = L[k];
+                C[k] = L1[k];  // (loaded with the rest of line 0, above)
             open_block(1, true);
             blk = 2;
             for (u32 k = 1; 2u * k + 1u < nfull; k++) {
@@ -1868,7 +1950,9 @@ enum Staging { ST_DIRECT = 0, ST_LINES = 1, ST_REGION = 2, ST_SHIFT = 3 };
 // -> slot out[i*out_stride .. +out_stride), nonce counter0 + i, flags8[i] (or 0).
 // ST_LINES / ST_REGION need the launcher's preconditions (see czk_seal_uniform);
 // a wave with fewer than 64 frames always stores directly.
-template <int ST, bool PAIR>
+// MODE_BOX (cz_seal_uniform_box): frame i = the box at in + i*in_stride (len = payload bytes),
+// flags from box byte 32, flags8 unused.
+template <int ST, bool PAIR, int MODE = MODE_ZMQ>
 __global__ __launch_bounds__(BLOCK) CZ_OCC void k_seal_uniform(const uint8_t *__restrict__ in, uint64_t in_stride,
                                                          uint8_t *__restrict__ out, uint64_t out_stride,
                                                          uint32_t count, uint32_t len,
@@ -1895,16 +1979,16 @@ __global__ __launch_bounds__(BLOCK) CZ_OCC void k_seal_uniform(const uint8_t *__
     // high nonce word uniform over the wave (true unless the counters cross a 2^32 boundary)
     const bool un0 = allow_un0 && wave_uniform((u32)((counter0 + i) >> 32));
     if (ST != ST_DIRECT && full_wave) {
-        const u32 fl = flags8 ? flags8[i] : 0u;
+        const u32 fl = (MODE == MODE_ZMQ && flags8) ? flags8[i] : 0u;
         const u32 lane = threadIdx.x & 63u;
         if constexpr (ST == ST_LINES) {
             EmitLines em{smem + (threadIdx.x >> 6) * (LINE_LDS_BYTES / 16), out + (uint64_t)wave_first * out_stride,
                          dst, out_stride, lane, mlen, 0u, true,
                          smem + (WAVES * LINE_LDS_BYTES + (threadIdx.x >> 6) * HOLD_LDS_BYTES) / 16};
             if (un0)
-                seal_frame<MODE_ZMQ, true, EmitLines, PAIR, true>(src, len, fl, counter0 + i, key, em);
+                seal_frame<MODE, true, EmitLines, PAIR, true>(src, len, fl, counter0 + i, key, em);
             else
-                seal_frame<MODE_ZMQ, true, EmitLines, PAIR, false>(src, len, fl, counter0 + i, key, em);
+                seal_frame<MODE, true, EmitLines, PAIR, false>(src, len, fl, counter0 + i, key, em);
         } else if constexpr (ST == ST_SHIFT) {
             // bodies at any byte offset (dense packing, wire layout): byte-shifted line staging
             EmitShiftLinesUni em{reinterpret_cast<uint8_t *>(smem) + (threadIdx.x >> 6) * SHIFT_LDS_BYTES, dst, lane,
@@ -1912,32 +1996,32 @@ __global__ __launch_bounds__(BLOCK) CZ_OCC void k_seal_uniform(const uint8_t *__
             em.init(true);
             em.init_uniform(i - blockIdx.x * BLOCK, (u32)out_stride, out + (uint64_t)blockIdx.x * BLOCK * out_stride);
             if (un0)
-                seal_frame<MODE_ZMQ, true, EmitShiftLinesUni, PAIR, true>(src, len, fl, counter0 + i, key, em);
+                seal_frame<MODE, true, EmitShiftLinesUni, PAIR, true>(src, len, fl, counter0 + i, key, em);
             else
-                seal_frame<MODE_ZMQ, true, EmitShiftLinesUni, PAIR, false>(src, len, fl, counter0 + i, key, em);
+                seal_frame<MODE, true, EmitShiftLinesUni, PAIR, false>(src, len, fl, counter0 + i, key, em);
         } else {
             const u32 st = (u32)out_stride;
             EmitRegion em{smem + (threadIdx.x >> 6) * ((64u * st) >> 4), out + (uint64_t)wave_first * out_stride, st,
                           lane, mlen};
             if (un0)
-                seal_frame<MODE_ZMQ, true, EmitRegion, PAIR, true>(src, len, fl, counter0 + i, key, em);
+                seal_frame<MODE, true, EmitRegion, PAIR, true>(src, len, fl, counter0 + i, key, em);
             else
-                seal_frame<MODE_ZMQ, true, EmitRegion, PAIR, false>(src, len, fl, counter0 + i, key, em);
+                seal_frame<MODE, true, EmitRegion, PAIR, false>(src, len, fl, counter0 + i, key, em);
         }
         return;
     }
     if (i >= count)
         return;
-    const u32 fl = flags8 ? flags8[i] : 0u;
+    const u32 fl = (MODE == MODE_ZMQ && flags8) ? flags8[i] : 0u;
     if (aligned16(src, dst)) {
         EmitDirect<true> em{dst, mlen};
-        seal_frame<MODE_ZMQ, true, EmitDirect<true>, PAIR>(src, len, fl, counter0 + i, key, em);
+        seal_frame<MODE, true, EmitDirect<true>, PAIR>(src, len, fl, counter0 + i, key, em);
     } else if ((((uintptr_t)src) & 15u) == 0) {
         EmitDirect<false> em{dst, mlen};
-        seal_frame<MODE_ZMQ, true, EmitDirect<false>, PAIR>(src, len, fl, counter0 + i, key, em);
+        seal_frame<MODE, true, EmitDirect<false>, PAIR>(src, len, fl, counter0 + i, key, em);
     } else {
         EmitDirect<false> em{dst, mlen};
-        seal_frame<MODE_ZMQ, false>(src, len, fl, counter0 + i, key, em);
+        seal_frame<MODE, false>(src, len, fl, counter0 + i, key, em);
     }
 }
 
@@ -2027,7 +2111,12 @@ __global__ __launch_bounds__(BLOCK) CZ_OCC void k_open_uniform(const uint8_t *__
     u64 nonce = 0;
     u32 st;
     if (ST != ST_DIRECT && full_wave) {
-        long long floor = i > 0 ? (long long)read_be64(src - in_stride + 8) : (long long)floor0;
+        // (16-byte aligned slots here: the previous body's nonce is one 8-byte load, not 8 byte loads)
+        long long floor = (long long)floor0;
+        if (i > 0) {
+            const uint2 pn = *reinterpret_cast<const uint2 *>(src - in_stride + 8);
+            floor = (long long)(((u64)bswap32(pn.x) << 32) | (u64)bswap32(pn.y));
+        }
         const u32 lane = threadIdx.x & 63u;
         const bool un0 = allow_un0 && wave_uniform(*reinterpret_cast<const u32 *>(src + 8));
         if constexpr (ST == ST_LINES) {
@@ -2465,6 +2554,204 @@ __global__ __launch_bounds__(64) void k_box_nacl(const uint8_t *__restrict__ in,
     }
 }
 
+// ---- one NaCl box per launch (the jnacl crypto_box_afternm / open_afternm drop-ins) ----------
+// One call used to be a chain of copies and launches (subkey, segments, combine, wipe): ~50 us at
+// 4 KiB against ~11 us for a bare launch + sync (tools/diag/latency_ub.hip).  This kernel does the
+// whole call in ONE launch of one 256-thread workgroup, reading its input from and writing its
+// output to the caller thread's pinned staging (host memory the device addresses directly):
+//   - the subkey HSalsa20(k, n[0:16]) comes from the thread's device cache, or is derived here and
+//     cached (CurveZMQ uses one (k, "CurveZMQMESSAGE?") pair per connection direction);
+//   - thread t owns box blocks [t*w, t*w + w) (w <= NACL_ONE_W): loads them, XORs its keystream,
+//     writes the output and keeps the ciphertext for the MAC;
+//   - Poly1305 over c[32:len) in parallel: each thread runs Horner over its own 16-byte blocks
+//     (box block b >= 1 holds MAC blocks 4b-2 .. 4b+1), the full threads' partials are joined by a
+//     pairwise tree with multipliers r^(Q*2^l), Q = 4w MAC blocks per thread (radix 2^26), and the
+//     thread holding the last block continues its Horner chain from the joined value.
+// Staging layout (bytes): [0,32) k  [32,56) n  [56,60) rc (written here)  [128, 128 + len) input,
+// [out_off, out_off + len) output.  Seal: bytes 0..31 of m are not read (the host checked they are 0)
+// and the output holds c[16:len) at out_off + 16; open: the output holds m[32:len) at out_off + 32,
+// released by the host only when rc == 0.
+constexpr int NACL_ONE_T = 256;
+constexpr int NACL_ONE_W = 5;  // blocks per thread: boxes up to 256 * 5 * 64 = 80 KiB
+__global__ __launch_bounds__(NACL_ONE_T) void k_nacl_one(uint8_t *st, uint32_t len, int open, uint8_t *subcache,
+                                                         int miss, uint32_t out_off)
+{
+    __shared__ u32 s_key[8];       // subkey
+    __shared__ u32 s_rs[8];        // Poly1305 r (clamped) and s
+    __shared__ u32 s_tree[NACL_ONE_T * 5];
+    const u32 t = threadIdx.x;
+    const u32 nblk = (len + 63u) >> 6;
+    const u32 w = (nblk + NACL_ONE_T - 1) / NACL_ONE_T;
+    const u32 n0 = *reinterpret_cast<const u32 *>(st + 48), n1 = *reinterpret_cast<const u32 *>(st + 52);
+    if (t < 64) {  // wave 0: the subkey (every lane the same HSalsa20; lane 0 publishes it)
+        u32 key[8];
+        if (miss) {
+            u32 k[8];
+            const uint4 a = *reinterpret_cast<const uint4 *>(st), b = *reinterpret_cast<const uint4 *>(st + 16);
+            k[0] = a.x; k[1] = a.y; k[2] = a.z; k[3] = a.w; k[4] = b.x; k[5] = b.y; k[6] = b.z; k[7] = b.w;
+            const uint4 q = *reinterpret_cast<const uint4 *>(st + 32);
+            const u32 in4[4] = {q.x, q.y, q.z, q.w};
+            hsalsa20(key, k, in4);
+            if (t == 0) {
+                *reinterpret_cast<uint4 *>(subcache) = make_uint4(key[0], key[1], key[2], key[3]);
+                *reinterpret_cast<uint4 *>(subcache + 16) = make_uint4(key[4], key[5], key[6], key[7]);
+            }
+        } else {
+            load_key(subcache, key);
+        }
+        if (t < 8)
+            s_key[t] = key[t];
+    }
+    __syncthreads();
+    u32 key[8];
+#pragma unroll
+    for (int i = 0; i < 8; i++)
+        key[i] = s_key[i];
+    // keystream, XOR, output; the ciphertext of owned blocks stays in registers for the MAC
+    u32 Cb[NACL_ONE_W][16];
+    const u32 b0 = t * w;
+    const uint8_t *in = st + 128;
+    uint8_t *out = st + out_off;
+#pragma unroll
+    for (int j = 0; j < NACL_ONE_W; j++) {
+        const u32 b = b0 + (u32)j;
+        if ((u32)j >= w || b >= nblk)
+            continue;
+        u32 x[16];
+        salsa20_block<false>(x, key, n0, n1, b, 0u);
+        if (b == 0) {
+#pragma unroll
+            for (int i = 0; i < 4; i++)
+                s_rs[i] = x[i] & (i == 0 ? 0x0fffffffu : 0x0ffffffcu);
+#pragma unroll
+            for (int i = 4; i < 8; i++)
+                s_rs[i] = x[i];
+        }
+        const u32 o = 64u * b;
+        const u32 nb = len - o < 64u ? len - o : 64u;  // valid bytes of this block
+        u32 M[16];
+#pragma unroll
+        for (int c = 0; c < 4; c++) {
+            const u32 oc = o + 16u * c;
+            V4 v = (oc >= 32u || b != 0) ? ld16<true>(in + oc, oc < len ? len - oc : 0) : zero4();
+            M[4 * c] = v.x; M[4 * c + 1] = v.y; M[4 * c + 2] = v.z; M[4 * c + 3] = v.w;
+        }
+#pragma unroll
+        for (int k = 0; k < 16; k++) {
+            const u32 X = M[k] ^ x[k];
+            Cb[j][k] = open ? M[k] : X;  // the MAC runs over the ciphertext
+            M[k] = X;                    // output: c (seal) or m (open)
+        }
+        // output bytes [max(o, 32), o + nb) (seal: bytes 16..31 are the tag, written below)
+#pragma unroll
+        for (int c = 0; c < 4; c++) {
+            const u32 oc = o + 16u * c;
+            if (oc >= 32u && oc < len) {
+                const u32 cnt = len - oc < 16u ? len - oc : 16u;
+                if (cnt == 16u)
+                    *reinterpret_cast<uint4 *>(out + oc) = make_uint4(M[4 * c], M[4 * c + 1], M[4 * c + 2], M[4 * c + 3]);
+                else
+                    st_bytes(out + oc, M[4 * c], M[4 * c + 1], M[4 * c + 2], M[4 * c + 3], cnt);
+            }
+        }
+        (void)nb;
+    }
+    __syncthreads();
+    Poly P;
+    poly_init(P, s_rs[0], s_rs[1], s_rs[2], s_rs[3], s_rs[4], s_rs[5], s_rs[6], s_rs[7]);
+    // MAC blocks: p covers c[32 + 16p, 48 + 16p); NP of them, the last one possibly partial
+    const u32 mlen = len;
+    const u32 NP = mlen > 32u ? (mlen - 32u + 15u) >> 4 : 0u;
+    const u32 last_blk = nblk ? nblk - 1u : 0u;
+    const u32 L = last_blk / w;  // the thread holding the last box block
+    // Horner over this thread's MAC blocks, h = sum m_p r^(end - p)
+    auto horner = [&]() {
+#pragma unroll
+        for (int j = 0; j < NACL_ONE_W; j++) {
+            const u32 b = b0 + (u32)j;
+            if ((u32)j >= w || b >= nblk)
+                continue;
+#pragma unroll
+            for (int c = 0; c < 4; c++) {
+                const u32 oc = 64u * b + 16u * c;
+                if (oc < 32u || oc >= mlen)
+                    continue;
+                const u32 cnt = mlen - oc;
+                if (cnt >= 16u)
+                    poly_block(P, Cb[j][4 * c], Cb[j][4 * c + 1], Cb[j][4 * c + 2], Cb[j][4 * c + 3], 1u);
+                else
+                    poly_block_partial(P, Cb[j][4 * c], Cb[j][4 * c + 1], Cb[j][4 * c + 2], Cb[j][4 * c + 3], cnt);
+            }
+        }
+    };
+    if (t < L)
+        horner();
+    // join the full threads 0..L-1: G = sum_u A_u R0^u, u = L-1-t, by pairs with R_l = r^(Q 2^l)
+    const u32 Q = 4u * w;
+    F26 R = f26_from32(P.r0, P.r1, P.r2, P.r3, 0u);
+    {
+        F26 acc = R;  // r^Q by square-and-multiply, Q <= 20 (the same in every thread)
+        F26 base = R;
+        bool have = false;
+        for (u32 e = Q; e; e >>= 1) {
+            if (e & 1u) {
+                acc = have ? f26_mul(acc, base) : base;
+                have = true;
+            }
+            if (e > 1u)
+                base = f26_mul(base, base);
+        }
+        R = acc;
+    }
+    const u32 u = L - 1u - t;  // (meaningful for t < L)
+    F26 A = f26_from32(P.h0, P.h1, P.h2, P.h3, P.h4);
+    if (t < L) {
+#pragma unroll
+        for (int i = 0; i < 5; i++)
+            s_tree[u * 5 + i] = A.l[i];
+    }
+    for (u32 step = 1; step < L; step <<= 1) {
+        __syncthreads();
+        const bool act = t < L && (u % (2u * step)) == 0u && u + step < L;
+        F26 B;
+        if (act) {
+#pragma unroll
+            for (int i = 0; i < 5; i++)
+                B.l[i] = s_tree[(u + step) * 5 + i];
+            A = f26_add(A, f26_mul(B, R));
+        }
+        __syncthreads();
+        if (act) {
+#pragma unroll
+            for (int i = 0; i < 5; i++)
+                s_tree[u * 5 + i] = A.l[i];
+        }
+        R = f26_mul(R, R);
+    }
+    __syncthreads();
+    if (t == L) {
+        if (L > 0) {
+            F26 G;
+#pragma unroll
+            for (int i = 0; i < 5; i++)
+                G.l[i] = s_tree[i];  // u = 0
+            f26_to32(G, P.h0, P.h1, P.h2, P.h3, P.h4);
+        }
+        horner();  // continues from G: H = G r^(len_L) + h_L
+        u32 tag[4];
+        poly_finish(P, tag);
+        int rc = 0;
+        if (!open) {
+            *reinterpret_cast<uint4 *>(out + 16) = make_uint4(tag[0], tag[1], tag[2], tag[3]);
+        } else {
+            const uint4 tin = *reinterpret_cast<const uint4 *>(in + 16);
+            rc = ((tag[0] ^ tin.x) | (tag[1] ^ tin.y) | (tag[2] ^ tin.z) | (tag[3] ^ tin.w)) ? -1 : 0;
+        }
+        (void)NP;
+        *reinterpret_cast<int *>(st + 56) = rc;
+    }
+}
+
 // subkeys[i] = HSalsa20(precom[i], prefix16)
 __global__ __launch_bounds__(BLOCK) void k_subkeys(const uint8_t *__restrict__ precom, uint8_t *__restrict__ out,
                                                     uint32_t nkeys, uint32_t p0, uint32_t p1, uint32_t p2, uint32_t p3)
@@ -2593,6 +2880,27 @@ hipError_t czk_seal_uniform(const void *in, uint64_t in_stride, void *out, uint6
     return hipGetLastError();
 }
 
+// Box-layout input (MODE_BOX): whole-line staging for 128-byte multiple output slots, direct
+// stores otherwise; whole-line input loads always (the box is read where it lies).
+hipError_t czk_seal_uniform_box(const void *in, uint64_t in_stride, void *out, uint64_t out_stride, uint32_t count,
+                                uint32_t len, const void *subkey, uint64_t counter0, hipStream_t s)
+{
+    if (count == 0)
+        return hipSuccess;
+    dim3 grid((count + BLOCK - 1) / BLOCK);
+    const bool al = ((((uintptr_t)in | in_stride | (uintptr_t)out | out_stride) & 15u) == 0);
+    const int st = pick_staging(out_stride, len + 33u, al);
+    if (st == ST_LINES)
+        hipLaunchKernelGGL((k_seal_uniform<ST_LINES, true, MODE_BOX>), grid, dim3(BLOCK),
+                           WAVES * (LINE_LDS_BYTES + HOLD_LDS_BYTES), s, (const uint8_t *)in, in_stride, (uint8_t *)out,
+                           out_stride, count, len, (const uint8_t *)subkey, counter0, nullptr, g_un0);
+    else
+        hipLaunchKernelGGL((k_seal_uniform<ST_DIRECT, true, MODE_BOX>), grid, dim3(BLOCK), 0, s, (const uint8_t *)in,
+                           in_stride, (uint8_t *)out, out_stride, count, len, (const uint8_t *)subkey, counter0, nullptr,
+                           g_un0);
+    return hipGetLastError();
+}
+
 hipError_t czk_seal_desc(const cz_frame_desc *desc, const uint32_t *order, uint32_t count, const void *in, void *out,
                          const void *subkeys, hipStream_t s)
 {
@@ -2648,6 +2956,17 @@ hipError_t czk_box_nacl(const void *in, void *out, uint32_t len, const void *sub
                        (const uint8_t *)subkey, counter, open, rc);
     return hipGetLastError();
 }
+
+hipError_t czk_nacl_one(void *st, uint32_t len, int open, void *subcache, int miss, uint32_t out_off, hipStream_t s)
+{
+    if (len < 32u || (len + 63u) / 64u > (uint32_t)(NACL_ONE_T * NACL_ONE_W))
+        return hipErrorInvalidValue;
+    hipLaunchKernelGGL(k_nacl_one, dim3(1), dim3(NACL_ONE_T), 0, s, (uint8_t *)st, len, open, (uint8_t *)subcache, miss,
+                       out_off);
+    return hipGetLastError();
+}
+
+uint32_t czk_nacl_one_max(void) { return (uint32_t)(NACL_ONE_T * NACL_ONE_W * 64); }
 
 hipError_t czk_subkeys(const void *precom, void *out, uint32_t nkeys, const uint8_t prefix[16], hipStream_t s)
 {

@@ -384,6 +384,38 @@ def test_nacl_box_afternm_golden(L, torch_dev):
     assert cv.afternm(bytearray(31), bytes(31), 31, bytes(24), bytes(32)) == -1
 
 
+def test_nacl_one_launch_contract_and_subkey_cache(L, torch_dev):
+    """The one-launch drop-in (k_nacl_one): NaCl's ZEROBYTES contract -- a seal of an m whose first
+    32 bytes are not zero returns -1 (NaCl would key the MAC with them; the device path does not),
+    output untouched; the per-thread subkey cache -- 12 keys cycled through the 8-entry cache,
+    the same key under two nonce prefixes (client / server direction), cz_nacl_forget in between --
+    never serves a stale subkey: every box against the oracle."""
+    from cz_testlib import or_box_afternm
+    lib = L.lib()
+    rng = np.random.default_rng(5)
+    m = bytearray(32 + 100)
+    m[32:] = rng.integers(0, 256, 100, dtype=np.uint8).tobytes()
+    m[5] = 1
+    c = ctypes.create_string_buffer(b"\x5a" * len(m), len(m))
+    assert lib.cz_box_afternm(c, bytes(m), len(m), bytes(24), bytes(32)) == -1
+    assert c.raw == b"\x5a" * len(m)
+    keys = [rng.integers(0, 256, 32, dtype=np.uint8).tobytes() for _ in range(12)]
+    for rnd in range(3):
+        for i, key in enumerate(keys):
+            for prefix in (b"CurveZMQMESSAGEC", b"CurveZMQMESSAGES"):
+                n24 = prefix + (1000 * rnd + i).to_bytes(8, "big")
+                mlen = 32 + 1 + int(rng.integers(0, 6000))
+                mm = bytes(32) + rng.integers(0, 256, mlen - 32, dtype=np.uint8).tobytes()
+                rc, want = or_box_afternm(mm, n24, key)
+                assert rc == 0
+                cc = ctypes.create_string_buffer(mlen)
+                assert lib.cz_box_afternm(cc, mm, mlen, n24, key) == 0 and cc.raw == want, (rnd, i, mlen)
+                back = ctypes.create_string_buffer(mlen)
+                assert lib.cz_box_open_afternm(back, want, mlen, n24, key) == 0 and back.raw == mm
+        if rnd == 1:
+            assert lib.cz_nacl_forget() == 0
+
+
 def test_nacl_single_shot_multi_lane(L, torch_dev):
     """The jnacl drop-ins (Curve.java:129-147) for one message of any size: large boxes run through the
     segment kernels (many lanes); every byte and tag against the oracle (NaCl secretbox), m[32] any

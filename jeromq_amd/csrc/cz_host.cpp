@@ -27,7 +27,7 @@ hipError_t czk_open_desc(const cz_frame_desc *, const uint32_t *, uint32_t, cons
 hipError_t czk_open_uniform(const void *, uint64_t, void *, uint64_t, uint32_t, uint32_t, const void *, uint64_t, int,
                             uint16_t *, hipStream_t);
 hipError_t czk_box_nacl(const void *, void *, uint32_t, const void *, uint64_t, int, int *, hipStream_t);
-hipError_t czk_nacl_one(void *, uint32_t, int, void *, int, uint32_t, hipStream_t);
+hipError_t czk_nacl_one(void *, uint32_t, int, void *, int, uint32_t, const uint8_t *, const uint8_t *, hipStream_t);
 uint32_t czk_nacl_one_max(void);
 hipError_t czk_fill(void *, uint64_t, uint64_t, hipStream_t);
 hipError_t czk_copy16(void *, const void *, uint64_t, hipStream_t);
@@ -125,14 +125,15 @@ struct Single {
     uint8_t ckey[NCACHE][48] = {};  // k || n[0:16] of each cached subkey
     bool cvalid[NCACHE] = {};
     int cnext = 0;
-    ~Single() { forget_host(); }
-    void forget_host()
+    // (the destructor touches no HIP memory: at process exit the runtime may be gone first)
+    ~Single() { forget_host(false); }
+    void forget_host(bool staging)
     {
         explicit_bzero(ckey, sizeof ckey);
         for (bool &v : cvalid)
             v = false;
-        if (one.ptr)
-            explicit_bzero(one.ptr, 64);
+        if (staging && one.ptr)
+            explicit_bzero(one.ptr, one.cap);
     }
 };
 
@@ -197,22 +198,17 @@ static int nacl_one_launch(uint8_t *dst, const uint8_t *src, uint64_t len, const
         memcpy(s.ckey[slot], k, 32);
         memcpy(s.ckey[slot] + 32, n, 16);
         s.cvalid[slot] = false;  // valid once the launch that derives it has completed
-        memcpy(st, k, 32);
     }
-    memcpy(st + 32, n, 24);
     memcpy(st + 128, src, len);
     *(volatile int *)(st + 56) = -2;
-    if ((e = czk_nacl_one(st, (uint32_t)len, open, (uint8_t *)s.subcache.ptr + 32 * slot, miss, (uint32_t)out_off,
+    if ((e = czk_nacl_one(st, (uint32_t)len, open, (uint8_t *)s.subcache.ptr + 32 * slot, miss, (uint32_t)out_off, k, n,
                           s.stream)) != hipSuccess ||
         (e = hipStreamSynchronize(s.stream)) != hipSuccess) {
-        explicit_bzero(st, 32);
         hip_fail(e, "cz_box (one launch)");
         return -1;
     }
-    if (miss) {
-        explicit_bzero(st, 32);
+    if (miss)
         s.cvalid[slot] = true;
-    }
     const int rc = *(volatile int *)(st + 56);
     if (!open) {
         memset(dst, 0, 16);
@@ -491,7 +487,7 @@ int cz_box_afternm(uint8_t *c, const uint8_t *m, uint64_t mlen, const uint8_t n[
 int cz_nacl_forget(void)
 {
     Single &s = t_single;
-    s.forget_host();
+    s.forget_host(true);
     if (s.ready && s.subcache.ptr) {
         hipError_t e = hipMemsetAsync(s.subcache.ptr, 0, s.subcache.cap, s.stream);
         if (e == hipSuccess)

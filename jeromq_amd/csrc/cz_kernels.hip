@@ -2567,14 +2567,20 @@ __global__ __launch_bounds__(64) void k_box_nacl(const uint8_t *__restrict__ in,
 //     (box block b >= 1 holds MAC blocks 4b-2 .. 4b+1), the full threads' partials are joined by a
 //     pairwise tree with multipliers r^(Q*2^l), Q = 4w MAC blocks per thread (radix 2^26), and the
 //     thread holding the last block continues its Horner chain from the joined value.
-// Staging layout (bytes): [0,32) k  [32,56) n  [56,60) rc (written here)  [128, 128 + len) input,
-// [out_off, out_off + len) output.  Seal: bytes 0..31 of m are not read (the host checked they are 0)
+// k and n come in the kernel arguments; staging layout (bytes): [56,60) rc (written here),
+// [128, 128 + len) input, [out_off, out_off + len) output.  Seal: bytes 0..31 of m are not read (the host checked they are 0)
 // and the output holds c[16:len) at out_off + 16; open: the output holds m[32:len) at out_off + 32,
 // released by the host only when rc == 0.
 constexpr int NACL_ONE_T = 256;
 constexpr int NACL_ONE_W = 5;  // blocks per thread: boxes up to 256 * 5 * 64 = 80 KiB
+// k and n travel in the kernel arguments (the dispatch packet), not through host memory: the only
+// PCIe read on the critical path is the message itself, issued first
+struct NaclOneArgs {
+    u32 k[8];   // precom (used on a subkey-cache miss)
+    u32 n[6];   // the 24-byte nonce, little-endian words
+};
 __global__ __launch_bounds__(NACL_ONE_T) void k_nacl_one(uint8_t *st, uint32_t len, int open, uint8_t *subcache,
-                                                         int miss, uint32_t out_off)
+                                                         int miss, uint32_t out_off, NaclOneArgs args)
 {
     __shared__ u32 s_key[8];       // subkey
     __shared__ u32 s_rs[8];        // Poly1305 r (clamped) and s
@@ -2582,16 +2588,30 @@ __global__ __launch_bounds__(NACL_ONE_T) void k_nacl_one(uint8_t *st, uint32_t l
     const u32 t = threadIdx.x;
     const u32 nblk = (len + 63u) >> 6;
     const u32 w = (nblk + NACL_ONE_T - 1) / NACL_ONE_T;
-    const u32 n0 = *reinterpret_cast<const u32 *>(st + 48), n1 = *reinterpret_cast<const u32 *>(st + 52);
-    if (t < 64) {  // wave 0: the subkey (every lane the same HSalsa20; lane 0 publishes it)
+    const u32 n0 = args.n[4], n1 = args.n[5];
+    const u32 b0 = t * w;
+    const uint8_t *in = st + 128;
+    uint8_t *out = st + out_off;
+    // 1. this thread's message blocks (host memory, over PCIe): loads issued before anything else
+    u32 Cb[NACL_ONE_W][16];
+#pragma unroll
+    for (int j = 0; j < NACL_ONE_W; j++) {
+        const u32 b = b0 + (u32)j;
+        if ((u32)j >= w || b >= nblk)
+            continue;
+#pragma unroll
+        for (int c = 0; c < 4; c++) {
+            const u32 oc = 64u * b + 16u * c;
+            V4 v = (oc >= 32u) ? ld16<true>(in + oc, oc < len ? len - oc : 0) : zero4();
+            Cb[j][4 * c] = v.x; Cb[j][4 * c + 1] = v.y; Cb[j][4 * c + 2] = v.z; Cb[j][4 * c + 3] = v.w;
+        }
+    }
+    // 2. the subkey: wave 0 derives it (every lane the same HSalsa20; lane 0 caches it) or loads it
+    if (t < 64) {
         u32 key[8];
         if (miss) {
-            u32 k[8];
-            const uint4 a = *reinterpret_cast<const uint4 *>(st), b = *reinterpret_cast<const uint4 *>(st + 16);
-            k[0] = a.x; k[1] = a.y; k[2] = a.z; k[3] = a.w; k[4] = b.x; k[5] = b.y; k[6] = b.z; k[7] = b.w;
-            const uint4 q = *reinterpret_cast<const uint4 *>(st + 32);
-            const u32 in4[4] = {q.x, q.y, q.z, q.w};
-            hsalsa20(key, k, in4);
+            const u32 in4[4] = {args.n[0], args.n[1], args.n[2], args.n[3]};
+            hsalsa20(key, args.k, in4);
             if (t == 0) {
                 *reinterpret_cast<uint4 *>(subcache) = make_uint4(key[0], key[1], key[2], key[3]);
                 *reinterpret_cast<uint4 *>(subcache + 16) = make_uint4(key[4], key[5], key[6], key[7]);
@@ -2607,11 +2627,7 @@ __global__ __launch_bounds__(NACL_ONE_T) void k_nacl_one(uint8_t *st, uint32_t l
 #pragma unroll
     for (int i = 0; i < 8; i++)
         key[i] = s_key[i];
-    // keystream, XOR, output; the ciphertext of owned blocks stays in registers for the MAC
-    u32 Cb[NACL_ONE_W][16];
-    const u32 b0 = t * w;
-    const uint8_t *in = st + 128;
-    uint8_t *out = st + out_off;
+    // 3. keystream, XOR, output; Cb keeps the ciphertext for the MAC
 #pragma unroll
     for (int j = 0; j < NACL_ONE_W; j++) {
         const u32 b = b0 + (u32)j;
@@ -2628,21 +2644,14 @@ __global__ __launch_bounds__(NACL_ONE_T) void k_nacl_one(uint8_t *st, uint32_t l
                 s_rs[i] = x[i];
         }
         const u32 o = 64u * b;
-        const u32 nb = len - o < 64u ? len - o : 64u;  // valid bytes of this block
         u32 M[16];
 #pragma unroll
-        for (int c = 0; c < 4; c++) {
-            const u32 oc = o + 16u * c;
-            V4 v = (oc >= 32u || b != 0) ? ld16<true>(in + oc, oc < len ? len - oc : 0) : zero4();
-            M[4 * c] = v.x; M[4 * c + 1] = v.y; M[4 * c + 2] = v.z; M[4 * c + 3] = v.w;
-        }
-#pragma unroll
         for (int k = 0; k < 16; k++) {
-            const u32 X = M[k] ^ x[k];
-            Cb[j][k] = open ? M[k] : X;  // the MAC runs over the ciphertext
-            M[k] = X;                    // output: c (seal) or m (open)
+            M[k] = Cb[j][k] ^ x[k];  // output: c (seal) or m (open)
+            if (!open)
+                Cb[j][k] = M[k];     // the MAC runs over the ciphertext
         }
-        // output bytes [max(o, 32), o + nb) (seal: bytes 16..31 are the tag, written below)
+        // output bytes [max(o, 32), min(o + 64, len)) (seal: bytes 16..31 are the tag, written below)
 #pragma unroll
         for (int c = 0; c < 4; c++) {
             const u32 oc = o + 16u * c;
@@ -2654,7 +2663,6 @@ __global__ __launch_bounds__(NACL_ONE_T) void k_nacl_one(uint8_t *st, uint32_t l
                     st_bytes(out + oc, M[4 * c], M[4 * c + 1], M[4 * c + 2], M[4 * c + 3], cnt);
             }
         }
-        (void)nb;
     }
     __syncthreads();
     Poly P;
@@ -2957,12 +2965,19 @@ hipError_t czk_box_nacl(const void *in, void *out, uint32_t len, const void *sub
     return hipGetLastError();
 }
 
-hipError_t czk_nacl_one(void *st, uint32_t len, int open, void *subcache, int miss, uint32_t out_off, hipStream_t s)
+hipError_t czk_nacl_one(void *st, uint32_t len, int open, void *subcache, int miss, uint32_t out_off,
+                        const uint8_t k[32], const uint8_t n[24], hipStream_t s)
 {
     if (len < 32u || (len + 63u) / 64u > (uint32_t)(NACL_ONE_T * NACL_ONE_W))
         return hipErrorInvalidValue;
+    NaclOneArgs a;
+    __builtin_memcpy(a.k, k, 32);
+    __builtin_memcpy(a.n, n, 24);
     hipLaunchKernelGGL(k_nacl_one, dim3(1), dim3(NACL_ONE_T), 0, s, (uint8_t *)st, len, open, (uint8_t *)subcache, miss,
-                       out_off);
+                       out_off, a);
+    volatile u32 *vk = a.k;  // the launch copied the arguments: no key left on this stack frame
+    for (int i = 0; i < 8; i++)
+        vk[i] = 0u;
     return hipGetLastError();
 }
 

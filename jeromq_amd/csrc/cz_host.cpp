@@ -371,6 +371,8 @@ void plan_segments(const cz_frame_desc *h_desc, uint32_t count, int open, uint32
 {
     segs.clear();
     combs.clear();
+    // (split threshold 1.0 / 1.25 / 1.5 / 2.0 x seg_blocks measured within noise on the Zipf batch,
+    // profiles/r03/zipf_order_split_s7_s8.log)
     const uint32_t split_above = seg_blocks + seg_blocks / 2;
     segs.reserve(count);
     uint32_t parts = 0;

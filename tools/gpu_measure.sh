@@ -5,6 +5,8 @@
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 mkdir -p gpurun_out
 export TMPDIR=/tmp
+# PART=bench: tests, smoke, bench lines, kernel traces; PART=pmc: the PMC passes (each fits one gpurun call)
+if [ "${PART:-bench}" = bench ]; then
 echo "== pytest -m gpu"
 timeout -k 10 600 python -u -m pytest tests -m gpu -x -q --timeout 120 --timeout-method thread -p no:cacheprovider > gpurun_out/pytest_gpu.log 2>&1
 rc=$?; tail -2 gpurun_out/pytest_gpu.log; [ $rc -eq 0 ] || exit $rc
@@ -19,6 +21,7 @@ run() {  # name, bench args
 }
 run 4k --config 4k
 run 4k_dense --config 4k_dense --no-cpu-baseline
+run 4k_box --config 4k_box --no-cpu-baseline
 run 100b --config 100b --no-cpu-baseline
 run zipf --config zipf --no-cpu-baseline
 run zipf_oa8 --config zipf --in-align 8 --out-align 8 --no-cpu-baseline
@@ -28,10 +31,16 @@ run zipf_lane --config zipf_lane --no-cpu-baseline
 for cfg in e2e4k engine beforenm nacl; do
   run $cfg --steps 10 --warmup 2 --config $cfg --no-cpu-baseline
 done
-for cfg in 4k zipf open4k 100b 4k_dense; do
-  echo "== rocprofv3 kernel trace $cfg"
-  timeout -k 10 300 rocprofv3 --kernel-trace --stats -T --output-format csv -d gpurun_out/prof_$cfg -o run -- python3 bench.py --steps 10 --warmup 2 --no-cpu-baseline --no-roundtrip --config $cfg > gpurun_out/prof_$cfg.log 2>&1 || { tail gpurun_out/prof_$cfg.log; exit 6; }
+for key in 4k zipf open4k 100b 4k_dense 4k_box zipf@ia8,oa8 zipf@oa1; do
+  args=$(python3 tools/pmc_key.py args "$key"); f=$(python3 tools/pmc_key.py file "$key")
+  echo "== rocprofv3 kernel trace $key"
+  timeout -k 10 300 rocprofv3 --kernel-trace --stats -T --output-format csv -d gpurun_out/prof_$f -o run -- python3 bench.py --steps 10 --warmup 2 --no-cpu-baseline --no-roundtrip $args > gpurun_out/prof_$f.log 2>&1 || { tail gpurun_out/prof_$f.log; exit 6; }
 done
-bash tools/gpu_traffic.sh 4k 100b zipf open4k 4k_dense || exit 7
-bash tools/gpu_valu.sh 4k 100b zipf open4k 4k_dense || exit 8
+fi
+if [ "${PART:-bench}" = pmc ]; then
+bash tools/gpu_traffic.sh 4k 100b zipf open4k 4k_dense 4k_box zipf@oa1 || exit 7
+bash tools/gpu_valu.sh 4k 100b zipf open4k 4k_dense 4k_box zipf@ia8,oa8 zipf@oa1 || exit 8
+bash tools/gpu_stall.sh 4k open4k zipf > gpurun_out/stall_measure.log 2>&1 || { tail gpurun_out/stall_measure.log; exit 9; }
+cp profiles/pmc_traffic.json gpurun_out/pmc_traffic_measure.json
+fi
 exit 0

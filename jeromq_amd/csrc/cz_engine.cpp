@@ -30,6 +30,13 @@
 
 #include "cz_internal.h"
 
+// pipeline depth of a large flush: groups of >= 8 MiB of wire bytes, at most this many.  At 1 GiB
+// per flush, 16 against 8: out 39.0 -> 40.9, in 38.0 -> 40.0 GiB/s (shorter pipeline fill and
+// drain); 24 and 32 drop flush_out to 28 / 20 GiB/s (profiles/r03/engine_groups_ab_s9/s10.log).
+#ifndef CZ_ENGINE_GROUPS
+#define CZ_ENGINE_GROUPS 16
+#endif
+
 using namespace czi;
 
 namespace {
@@ -322,7 +329,7 @@ struct cz_engine {
         };
         std::vector<Group> groups;
         {
-            const uint64_t G = std::min<uint64_t>(8, std::max<uint64_t>(1, w / (8ull << 20)));
+            const uint64_t G = std::min<uint64_t>(CZ_ENGINE_GROUPS, std::max<uint64_t>(1, w / (8ull << 20)));
             uint32_t fa = 0;
             for (uint32_t i = 0; i < n; i++)
                 if (i + 1 == n || wpos[i + 1] * G >= w * (groups.size() + 1)) {
@@ -484,7 +491,7 @@ struct cz_engine {
         };
         std::vector<Group> groups;
         {
-            const int G = rx_total >= (64ull << 20) ? 8 : 1;
+            const int G = rx_total >= (64ull << 20) ? CZ_ENGINE_GROUPS : 1;
             size_t pa = 0;
             uint64_t acc = 0;
             for (size_t q = 0; q < parsed.size(); q++) {

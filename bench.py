@@ -58,6 +58,7 @@ def parse():
     ap.add_argument("--config", default="4k", choices=["4k", "4k_dense", "4k_box", "100b", "zipf", "zipf_lane", "open4k", "e2e4k",
                                                           "engine", "nacl", "beforenm"])
     ap.add_argument("--frames", type=int, default=FRAMES)
+    ap.add_argument("--chunk-frames", type=int, default=16384, help="e2e4k: frames per pipeline chunk")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-scatter", action="store_true",
                     help="N>1, 4k: skip the separately timed RCCL scatter -> seal -> gather leg")
@@ -393,7 +394,7 @@ def e2e_host(args, dev):
     ctx = ctypes.c_void_p()
     _lib.check(lib.cz_ctx_create(ctypes.byref(ctx), dev.index or 0), "cz_ctx_create")
     _lib.check(lib.cz_ctx_set_keys(ctx, PRECOM, 1, _lib.CZ_DIR_C2S), "cz_ctx_set_keys")
-    chunk = 16384
+    chunk = args.chunk_frames
     res = {}
     for name, fn in (("seal", lambda: lib.cz_ctx_seal_uniform(ctx, frames, n, pin, in_stride, pout, out_stride, 3,
                                                                None, chunk)),

@@ -555,8 +555,8 @@ def nacl_latency(args, dev):
     bmax = 1 << 16
     pin, pout = lib.cz_host_alloc(bmax * 4096), lib.cz_host_alloc(bmax * 4224)
     batches = []
-    for B in (1, 4, 16, 64, 256, 1024, 4096, 16384, 65536):
-        t = med(lambda: _lib.check(lib.cz_ctx_seal_uniform(ctx, B, 4096, pin, 4096, pout, 4224, 3, None, 16384),
+    for B in (1, 4, 16, 64, 256, 1024, 2048, 4096, 8192, 16384, 65536):
+        t = med(lambda: _lib.check(lib.cz_ctx_seal_uniform(ctx, B, 4096, pin, 4096, pout, 4224, 3, None, 0),
                                    "seal"), 100)
         batches.append({"batch": B, "call_us": round(t * 1e6, 1), "per_msg_us": round(t * 1e6 / B, 3),
                         "GiBps": round(B * 4096 / t / 2**30, 3)})

@@ -212,11 +212,15 @@ int cz_ctx_seal(cz_ctx *ctx, const cz_frame_desc *h_desc, uint32_t count, const 
 int cz_ctx_open(cz_ctx *ctx, const cz_frame_desc *h_desc, uint32_t count, const void *h_in, uint64_t in_bytes,
                 void *h_out, uint64_t out_bytes, uint16_t *h_status);
 /* Pipelined host-staged uniform batches (the end-to-end path at throughput): frames in
- * chunks of chunk_frames (0 = 16384); chunk k runs H2D -> kernel -> D2H on one of three
- * streams with its own device buffers, so PCIe copies in both directions overlap each
- * other and the kernels.  Host buffers should be pinned (cz_host_alloc) for full PCIe
- * rate; the output host buffer must span count * out_stride bytes (whole slots).  Uses
- * the context's key 0 (cz_ctx_set_keys).  Synchronous. */
+ * chunks of chunk_frames (0 = 16384); chunk k runs H2D -> kernel
+ * -> D2H on one of three streams with its own device buffers, so PCIe copies in both
+ * directions overlap each other and the kernels.  A batch that is one chunk of at most
+ * 64 MiB (in + out slots) of frames of 8+ blocks runs on one stream through the segment
+ * kernels instead, so a few frames cost tens of us rather than one lane's whole walk; it
+ * writes the bodies only and leaves slot padding as it was.  Rejected opens leave zeros in
+ * their payload slots.  Host buffers should be pinned (cz_host_alloc) for full PCIe rate;
+ * the output host buffer must span count * out_stride bytes (whole slots).  Uses the
+ * context's key 0 (cz_ctx_set_keys).  Synchronous. */
 int cz_ctx_seal_uniform(cz_ctx *ctx, uint32_t count, uint32_t len, const void *h_in, uint64_t in_stride, void *h_out,
                         uint64_t out_stride, uint64_t counter0, const uint8_t *h_flags8, uint32_t chunk_frames);
 int cz_ctx_open_uniform(cz_ctx *ctx, uint32_t count, uint32_t size, const void *h_in, uint64_t in_stride, void *h_out,

@@ -445,10 +445,15 @@ void plan_segments(const cz_frame_desc *h_desc, uint32_t count, int open, uint32
 using namespace czi;
 
 // ---- cz_ctx ----------------------------------------------------------------
+// host-staged uniform batches up to this many bytes (in + out slots) run on one stream
+constexpr uint64_t SMALL_BATCH_BYTES = 4ull << 20;
+// single-chunk host-staged uniform batches of multi-block frames up to this many bytes: segment kernels
+constexpr uint64_t SEG_BATCH_BYTES = 64ull << 20;
+
 struct cz_ctx {
     int device = 0;
     hipStream_t stream = nullptr;
-    DevBuf desc, in, out, status, keys, subkeys;
+    DevBuf desc, in, out, status, keys, subkeys, work;
     HostBuf hdesc;
     uint32_t nkeys = 0;
     // pipelined uniform batches: one stream per role (H2D, kernels, D2H) and NB chunk buffer sets
@@ -726,6 +731,7 @@ void cz_ctx_destroy(cz_ctx *c)
     c->status.release();
     c->keys.release();
     c->subkeys.release();
+    c->work.release();
     c->hdesc.release();
     for (int k = 0; k < cz_ctx::PIPE; k++)
         if (c->ps[k]) {
@@ -835,6 +841,80 @@ int cz_ctx_open(cz_ctx *c, const cz_frame_desc *h_desc, uint32_t count, const vo
     return ctx_run(c, h_desc, count, h_in, in_bytes, h_out, out_bytes, h_status, false);
 }
 
+// Host-staged uniform batch of one chunk (<= SEG_BATCH_BYTES) through the segment kernels.
+// The uniform kernel walks a frame's blocks on one lane, so a batch of a few frames costs one
+// lane's whole walk (~150 us at 4 KiB); segments of a few blocks spread each frame over many lanes.
+// Uniform frames need no sort: segments go out segment-major (segment s of every frame, then s + 1),
+// which keeps equal lengths together.
+static int ctx_uniform_segments(cz_ctx *c, bool seal, uint32_t count, uint32_t len, const void *h_in,
+                                uint64_t in_stride, void *h_out, uint64_t out_stride, uint64_t counter0,
+                                const uint8_t *h_flags8, uint16_t *h_status, int check, uint32_t nblk)
+{
+    const uint64_t olen = seal ? (uint64_t)len + CZ_MESSAGE_OVERHEAD : (uint64_t)len - CZ_MESSAGE_OVERHEAD;
+    if (count == 1) {  // strides are not checked for one frame
+        in_stride = len;
+        out_stride = std::max<uint64_t>(olen, 1);
+    }
+    uint32_t seg = std::max<uint32_t>(single_seg_blocks(nblk), (uint32_t)(((uint64_t)count * nblk + 65535) / 65536));
+    seg = std::min<uint32_t>(seg, 128);
+    const uint32_t lead = seal ? 0u : 1u;
+    const bool split = nblk > seg + seg / 2;
+    const uint32_t ns = split ? (nblk - lead + seg - 1) / seg : 1u;
+    const uint64_t nseg = (uint64_t)count * ns, ncomb = split ? count : 0;
+    const uint64_t m_desc = 0, m_seg = (uint64_t)count * sizeof(cz_frame_desc),
+                   m_comb = m_seg + nseg * sizeof(cz_segment), m_end = m_comb + ncomb * sizeof(cz_combine);
+    const uint64_t in_bytes = (uint64_t)(count - 1) * in_stride + len, out_bytes = (uint64_t)count * out_stride;
+    hipError_t e;
+    if ((e = c->hdesc.reserve(m_end)) != hipSuccess || (e = c->desc.reserve(m_end)) != hipSuccess ||
+        (e = c->in.reserve(in_bytes + 16)) != hipSuccess || (e = c->out.reserve(out_bytes + 16)) != hipSuccess ||
+        (e = c->status.reserve(2ull * count)) != hipSuccess ||
+        (e = c->work.reserve(64ull * std::max<uint64_t>(ncomb * ns, 1))) != hipSuccess)
+        return hip_fail(e, "alloc");
+    uint8_t *hm = (uint8_t *)c->hdesc.ptr;
+    cz_frame_desc *hd = (cz_frame_desc *)(hm + m_desc);
+    cz_segment *hs = (cz_segment *)(hm + m_seg);
+    cz_combine *hc = (cz_combine *)(hm + m_comb);
+    for (uint32_t i = 0; i < count; i++) {
+        if (seal)
+            hd[i] = {(uint64_t)i * in_stride, (uint64_t)i * out_stride, len, 0u, counter0 + i,
+                     h_flags8 ? (uint32_t)h_flags8[i] : 0u, -1};
+        else
+            hd[i] = {(uint64_t)i * in_stride, (uint64_t)i * out_stride, len, 0u, counter0,
+                     check ? (uint32_t)CZ_DESC_CHECK_NONCE : 0u, i ? (int32_t)(i - 1) : -1};
+    }
+    for (uint32_t s = 0; s < ns; s++) {
+        const uint32_t b0 = s ? s * seg + lead : 0u, b1 = s + 1 < ns ? (s + 1) * seg + lead : nblk;
+        for (uint32_t i = 0; i < count; i++)
+            hs[(uint64_t)s * count + i] = {i, b0, b1 - b0, split ? i * ns + s : 0xffffffffu};
+    }
+    for (uint64_t i = 0; i < ncomb; i++)
+        hc[i] = {(uint32_t)i, (uint32_t)i * ns, ns, 0u};
+    hipStream_t q = c->ps[1];
+    uint8_t *dm = (uint8_t *)c->desc.ptr;
+    const cz_frame_desc *dd = (const cz_frame_desc *)(dm + m_desc);
+    const cz_segment *ds = (const cz_segment *)(dm + m_seg);
+    const cz_combine *dc = (const cz_combine *)(dm + m_comb);
+    if ((e = hipMemcpyAsync(dm, hm, m_end, hipMemcpyHostToDevice, q)) != hipSuccess ||
+        (e = hipMemcpyAsync(c->in.ptr, h_in, in_bytes, hipMemcpyHostToDevice, q)) != hipSuccess)
+        return hip_fail(e, "H2D");
+    if (seal) {
+        e = czk_seal_segments(dd, ds, (uint32_t)nseg, dc, (uint32_t)ncomb, c->in.ptr, c->out.ptr, c->subkeys.ptr,
+                              c->work.ptr, q);
+    } else if ((e = hipMemsetAsync(c->out.ptr, 0, out_bytes, q)) == hipSuccess) {  // rejected frames: zeros
+        e = czk_open_segments(dd, ds, (uint32_t)nseg, dc, (uint32_t)ncomb, c->in.ptr, c->out.ptr, c->subkeys.ptr,
+                              c->work.ptr, (uint16_t *)c->status.ptr, nullptr, q);
+    }
+    if (e != hipSuccess)
+        return hip_fail(e, "launch");
+    // the bodies only: the caller's slot padding is left as it was
+    if ((olen && (e = hipMemcpy2DAsync(h_out, out_stride, c->out.ptr, out_stride, olen, count, hipMemcpyDeviceToHost,
+                                       q)) != hipSuccess) ||
+        (!seal && (e = hipMemcpyAsync(h_status, c->status.ptr, 2ull * count, hipMemcpyDeviceToHost, q)) != hipSuccess) ||
+        (e = hipStreamSynchronize(q)) != hipSuccess)
+        return hip_fail(e, "D2H");
+    return CZ_OK;
+}
+
 // Pipelined host-staged uniform batch.  Chunk k of `chunk` frames uses buffer set k % NB:
 //   stream 0: H2D of chunk k (after the kernel of chunk k - NB released the set's input)
 //   stream 1: kernel of chunk k (after its H2D, and after the D2H of chunk k - NB released the
@@ -857,6 +937,13 @@ static int ctx_uniform(cz_ctx *c, bool seal, uint32_t count, uint32_t len, const
         return fail(CZ_EINVAL, "cz_ctx_*_uniform: stride smaller than a frame");
     if (count == 0)
         return CZ_OK;
+    // a single-chunk batch of multi-block frames: the segment kernels (one stream)
+    const uint64_t nblk = ((seal ? (uint64_t)len + CZ_MESSAGE_OVERHEAD : (uint64_t)len) + 63) / 64;
+    static const bool lanes_only = getenv("CZ_CTX_LANES_ONLY") != nullptr;  // A/B: the lane-per-frame kernel
+    const bool seg_path = nblk >= 8 && (chunk == 0 || chunk >= count) && !lanes_only &&
+                          (uint64_t)count * (in_stride + out_stride) <= SEG_BATCH_BYTES;
+    // (default chunks of count / 8 within 2048 .. 16384 frames were slower than 16384 for every
+    // batch of 8192 .. 65536 x 4 KiB: profiles/r03/ctx_small_batch.log)
     if (chunk == 0)
         chunk = 16384;
     hipError_t e;
@@ -865,6 +952,9 @@ static int ctx_uniform(cz_ctx *c, bool seal, uint32_t count, uint32_t len, const
     for (int k = 0; k < cz_ctx::PIPE; k++)
         if (!c->ps[k] && (e = hipStreamCreateWithFlags(&c->ps[k], hipStreamNonBlocking)) != hipSuccess)
             return hip_fail(e, "hipStreamCreate");
+    if (seg_path)
+        return ctx_uniform_segments(c, seal, count, len, h_in, in_stride, h_out, out_stride, counter0, h_flags8,
+                                    h_status, check, (uint32_t)nblk);
     for (int k = 0; k < cz_ctx::NB; k++) {
         for (hipEvent_t *ev : {&c->ev_in[k], &c->ev_kern[k], &c->ev_out[k]})
             if (!*ev && (e = hipEventCreateWithFlags(ev, hipEventDisableTiming)) != hipSuccess)
@@ -877,6 +967,10 @@ static int ctx_uniform(cz_ctx *c, bool seal, uint32_t count, uint32_t len, const
     const uint8_t *hin = (const uint8_t *)h_in;
     uint8_t *hout = (uint8_t *)h_out;
     hipStream_t s_in = c->ps[0], s_k = c->ps[1], s_out = c->ps[2];
+    // A small batch runs H2D, kernel and D2H on one stream: each cross-stream event wait costs
+    // tens of us, which dominates below a few MiB (host-resident paths).
+    if (count == per && (uint64_t)count * (in_stride + out_stride) <= SMALL_BATCH_BYTES)
+        s_in = s_out = s_k;
     uint32_t k = 0;
     for (uint32_t f0 = 0; f0 < count; f0 += per, k++) {
         const uint32_t nc = count - f0 < per ? count - f0 : per;
@@ -893,9 +987,9 @@ static int ctx_uniform(cz_ctx *c, bool seal, uint32_t count, uint32_t len, const
                 return hip_fail(e, "H2D flags");
             dfl = (const uint8_t *)c->pflags[q].ptr;
         }
-        if ((e = hipEventRecord(c->ev_in[q], s_in)) != hipSuccess ||
-            (e = hipStreamWaitEvent(s_k, c->ev_in[q], 0)) != hipSuccess ||
-            (reuse && (e = hipStreamWaitEvent(s_k, c->ev_out[q], 0)) != hipSuccess))
+        if (s_in != s_k && ((e = hipEventRecord(c->ev_in[q], s_in)) != hipSuccess ||
+                            (e = hipStreamWaitEvent(s_k, c->ev_in[q], 0)) != hipSuccess ||
+                            (reuse && (e = hipStreamWaitEvent(s_k, c->ev_out[q], 0)) != hipSuccess)))
             return hip_fail(e, "event");
         if (seal) {
             e = czk_seal_uniform(c->pin[q].ptr, in_stride, c->pout[q].ptr, out_stride, nc, len, c->subkeys.ptr,
@@ -909,13 +1003,16 @@ static int ctx_uniform(cz_ctx *c, bool seal, uint32_t count, uint32_t len, const
                 for (int b = 0; b < 8; b++)
                     floor0 = (floor0 << 8) | pb[b];
             }
-            e = czk_open_uniform(c->pin[q].ptr, in_stride, c->pout[q].ptr, out_stride, nc, len, c->subkeys.ptr, floor0,
-                                 check, (uint16_t *)c->pstatus[q].ptr, s_k);
+            // zeros in rejected frames' slots, never an earlier chunk's plaintext
+            e = hipMemsetAsync(c->pout[q].ptr, 0, (uint64_t)nc * out_stride, s_k);
+            if (e == hipSuccess)
+                e = czk_open_uniform(c->pin[q].ptr, in_stride, c->pout[q].ptr, out_stride, nc, len, c->subkeys.ptr,
+                                     floor0, check, (uint16_t *)c->pstatus[q].ptr, s_k);
         }
         if (e != hipSuccess)
             return hip_fail(e, "launch");
-        if ((e = hipEventRecord(c->ev_kern[q], s_k)) != hipSuccess ||
-            (e = hipStreamWaitEvent(s_out, c->ev_kern[q], 0)) != hipSuccess)
+        if (s_out != s_k && ((e = hipEventRecord(c->ev_kern[q], s_k)) != hipSuccess ||
+                             (e = hipStreamWaitEvent(s_out, c->ev_kern[q], 0)) != hipSuccess))
             return hip_fail(e, "event");
         if ((e = hipMemcpyAsync(hout + (uint64_t)f0 * out_stride, c->pout[q].ptr, (uint64_t)nc * out_stride,
                                 hipMemcpyDeviceToHost, s_out)) != hipSuccess)
@@ -923,11 +1020,11 @@ static int ctx_uniform(cz_ctx *c, bool seal, uint32_t count, uint32_t len, const
         if (!seal && (e = hipMemcpyAsync(h_status + f0, c->pstatus[q].ptr, 2ull * nc, hipMemcpyDeviceToHost, s_out)) !=
                          hipSuccess)
             return hip_fail(e, "D2H status");
-        if ((e = hipEventRecord(c->ev_out[q], s_out)) != hipSuccess)
+        if (s_out != s_k && (e = hipEventRecord(c->ev_out[q], s_out)) != hipSuccess)
             return hip_fail(e, "event");
     }
     for (int q = 0; q < cz_ctx::PIPE; q++)
-        if ((e = hipStreamSynchronize(c->ps[q])) != hipSuccess)
+        if ((s_in != s_k || q == 1) && (e = hipStreamSynchronize(c->ps[q])) != hipSuccess)
             return hip_fail(e, "sync");
     return CZ_OK;
 }

@@ -539,9 +539,11 @@ def test_ctx_host_staged(L, torch_dev):
         lib.cz_ctx_destroy(ctx)
 
 
-def test_ctx_pipelined_uniform(L, torch_dev):
-    """Host-staged pipelined seal/open (3 streams, chunks) vs the oracle; chunk boundaries
-    carry the replay floor across chunks."""
+@pytest.mark.parametrize("chunk", [96, 0])
+def test_ctx_pipelined_uniform(L, torch_dev, chunk):
+    """Host-staged pipelined seal/open (3 streams, chunks of 96 frames) vs the oracle; chunk
+    boundaries carry the replay floor across chunks.  chunk=0: the default chunk holds the whole
+    688 KB batch, which runs on one stream (SMALL_BATCH_BYTES)."""
     lib = L.lib()
     ctx = ctypes.c_void_p()
     L.check(lib.cz_ctx_create(ctypes.byref(ctx), 0))
@@ -552,7 +554,7 @@ def test_ctx_pipelined_uniform(L, torch_dev):
         flags = (np.arange(count) % 3).astype(np.uint8)
         hout = np.zeros(count * ost, dtype=np.uint8)
         L.check(lib.cz_ctx_seal_uniform(ctx, count, n, hin.ctypes.data, ist, hout.ctypes.data, ost, 7,
-                                        flags.ctypes.data, 96))
+                                        flags.ctypes.data, chunk))
         for i in (0, 95, 96, 500, count - 1):
             body = hout[i * ost:i * ost + n + 33].tobytes()
             assert body == or_curve_encode(hin[i * ist:i * ist + n].tobytes(), int(flags[i]), 7 + i, 0, PRECOM)
@@ -560,7 +562,7 @@ def test_ctx_pipelined_uniform(L, torch_dev):
         st = np.zeros(count, dtype=np.uint16)
         L.check(lib.cz_ctx_set_keys(ctx, PRECOM, 1, L.CZ_DIR_C2S))
         L.check(lib.cz_ctx_open_uniform(ctx, count, n + 33, hout.ctypes.data, ost, back.ctypes.data, ist, 6, 1,
-                                        st.ctypes.data, 96))
+                                        st.ctypes.data, chunk))
         assert not np.any(st & 0xff)
         assert np.array_equal(st >> 8, flags)
         assert np.array_equal(back.reshape(count, ist)[:, :n], hin.reshape(count, ist)[:, :n])
@@ -568,8 +570,91 @@ def test_ctx_pipelined_uniform(L, torch_dev):
         hout2 = hout.copy()
         hout2[96 * ost + 8:96 * ost + 16] = hout2[95 * ost + 8:95 * ost + 16]
         L.check(lib.cz_ctx_open_uniform(ctx, count, n + 33, hout2.ctypes.data, ost, back.ctypes.data, ist, 6, 1,
-                                        st.ctypes.data, 96))
+                                        st.ctypes.data, chunk))
         assert (st[96] & 0xff) == L.CZ_STATUS_SEQUENCE and not np.any(st[:96] & 0xff)
+    finally:
+        lib.cz_ctx_destroy(ctx)
+
+
+def test_ctx_uniform_default_chunks(L, torch_dev):
+    """chunk_frames = 0 on a batch of frames too short for the segment path: 20000 x 100 B in
+    the default chunks of 16384 frames, three streams; frames around the chunk boundary against
+    the oracle and the whole open round trip, with the replay floor carried across chunks."""
+    lib = L.lib()
+    ctx = ctypes.c_void_p()
+    L.check(lib.cz_ctx_create(ctypes.byref(ctx), 0))
+    try:
+        L.check(lib.cz_ctx_set_keys(ctx, PRECOM, 1, L.CZ_DIR_C2S))
+        count, n, ist, ost = 20000, 100, 112, 144
+        hin = np.frombuffer(splitmix_bytes(count * ist, 4321), dtype=np.uint8).copy()
+        hout = np.zeros(count * ost, dtype=np.uint8)
+        L.check(lib.cz_ctx_seal_uniform(ctx, count, n, hin.ctypes.data, ist, hout.ctypes.data, ost, 5, None, 0))
+        for i in (0, 1, 16383, 16384, 16385, count - 1):
+            body = hout[i * ost:i * ost + n + 33].tobytes()
+            assert body == or_curve_encode(hin[i * ist:i * ist + n].tobytes(), 0, 5 + i, 0, PRECOM), i
+        back = np.zeros(count * ist, dtype=np.uint8)
+        st = np.full(count, 0xFFFF, dtype=np.uint16)
+        L.check(lib.cz_ctx_open_uniform(ctx, count, n + 33, hout.ctypes.data, ost, back.ctypes.data, ist, 4, 1,
+                                        st.ctypes.data, 0))
+        assert not np.any(st)
+        assert np.array_equal(back.reshape(count, ist)[:, :n], hin.reshape(count, ist)[:, :n])
+        bad = hout.copy()
+        e = 16384  # replay at the chunk edge
+        bad[e * ost + 8:e * ost + 16] = bad[(e - 1) * ost + 8:(e - 1) * ost + 16]
+        L.check(lib.cz_ctx_open_uniform(ctx, count, n + 33, bad.ctypes.data, ost, back.ctypes.data, ist, 4, 1,
+                                        st.ctypes.data, 0))
+        assert (st[e] & 0xff) == L.CZ_STATUS_SEQUENCE and np.count_nonzero(st) == 1
+        assert not back[e * ist:e * ist + n].any()
+    finally:
+        lib.cz_ctx_destroy(ctx)
+
+
+@pytest.mark.parametrize("count,n,ist,ost", [(300, 4096, 4096, 4224), (1, 4096, 0, 0), (64, 1000, 1000, 1033),
+                                             (7, 20000, 20000, 20040)])
+def test_ctx_uniform_small_segmented(L, torch_dev, count, n, ist, ost):
+    """Small host-staged uniform batches of multi-block frames (one chunk, <= 4 MiB) run the
+    segment kernels, segment-major: every body against the oracle, the caller's slot padding left
+    alone, the open round trip, and rejected frames (bad tag, replay, wrong command) with zeros in
+    their payload slots."""
+    lib = L.lib()
+    ctx = ctypes.c_void_p()
+    L.check(lib.cz_ctx_create(ctypes.byref(ctx), 0))
+    try:
+        L.check(lib.cz_ctx_set_keys(ctx, PRECOM, 1, L.CZ_DIR_C2S))
+        si, so = max(ist, n), max(ost, n + 33)
+        hin = np.frombuffer(splitmix_bytes(count * si, 77 + n), dtype=np.uint8).copy()
+        flags = (np.arange(count) % 3).astype(np.uint8)
+        hout = np.full(count * so, 0xCD, dtype=np.uint8)
+        L.check(lib.cz_ctx_seal_uniform(ctx, count, n, hin.ctypes.data, ist, hout.ctypes.data, ost, 11,
+                                        flags.ctypes.data, 0))
+        for i in range(count):
+            body = hout[i * so:i * so + n + 33].tobytes()
+            assert body == or_curve_encode(hin[i * si:i * si + n].tobytes(), int(flags[i]), 11 + i, 0, PRECOM), i
+            assert np.all(hout[i * so + n + 33:(i + 1) * so] == 0xCD), i
+        back = np.full(count * si, 0xEE, dtype=np.uint8)
+        st = np.full(count, 0xFFFF, dtype=np.uint16)
+        L.check(lib.cz_ctx_open_uniform(ctx, count, n + 33, hout.ctypes.data, ost, back.ctypes.data, ist, 10, 1,
+                                        st.ctypes.data, 0))
+        assert not np.any(st & 0xff)
+        assert np.array_equal(st >> 8, flags)
+        for i in range(count):
+            assert np.array_equal(back[i * si:i * si + n], hin[i * si:i * si + n]), i
+        if count < 64:
+            return
+        bad = hout.copy()
+        bad[5 * so + 100] ^= 1                                   # ciphertext -> CRYPTO
+        bad[17 * so + 8:17 * so + 16] = bad[16 * so + 8:16 * so + 16]  # replay -> SEQUENCE
+        bad[40 * so + 2] ^= 0x20                                 # "\x07MEsSAGE" -> COMMAND
+        back[:] = 0xEE
+        L.check(lib.cz_ctx_open_uniform(ctx, count, n + 33, bad.ctypes.data, ost, back.ctypes.data, ist, 10, 1,
+                                        st.ctypes.data, 0))
+        want = np.zeros(count, dtype=np.uint16)
+        want[5], want[17], want[40] = L.CZ_STATUS_CRYPTO, L.CZ_STATUS_SEQUENCE, L.CZ_STATUS_COMMAND
+        assert np.array_equal(st & 0xff, want), np.nonzero((st & 0xff) != want)
+        for i in (5, 17, 40):
+            assert not back[i * si:i * si + n].any(), i
+        for i in (4, 18, 41, count - 1):
+            assert np.array_equal(back[i * si:i * si + n], hin[i * si:i * si + n]), i
     finally:
         lib.cz_ctx_destroy(ctx)
 

@@ -478,6 +478,7 @@ def engine_host(args, dev):
     ok = ok and len(got) == per and got[-1][0] == payload[(per - 1) * n:per * n]
     ok = ok and all(srv.error(sc[c])[0] == 0 for c in range(nconn))
     msgs = nconn * per
+    small = engine_small_flush()
     ceil = copy_ceiling(dev)
     wire_bytes = sum(len(x) for x in wires)
     return {"metric": "CURVE batching engine end-to-end GiB/s (pinned host, 1024 connections, ZMTP v2 wire)",
@@ -487,7 +488,40 @@ def engine_host(args, dev):
             "open_GiBps": round(total / res["flush_in_s"] / 2**30, 3),
             "msgs_per_s_out": round(msgs / res["flush_out_s"], 1), "msgs_per_s_in": round(msgs / res["flush_in_s"], 1),
             "timings_s": {k: round(v, 4) for k, v in res.items()}, "verified": bool(ok),
+            "small_flush": small,
             "config": {"workload": f"{nconn} connections x {per} x {n} B MESSAGEs per flush", "frames": msgs}}
+
+
+def engine_small_flush(reps=60):
+    """Latency of small engine flushes: one connection, `count` MESSAGEs of `n` bytes per flush;
+    median wall clock of flush_out and of flush_in (the wire fed back to a server engine), with the
+    delivered payloads checked."""
+    from jeromq_amd.engine import CurveBatchEngine
+    rows = []
+    for count, n in ((1, 100), (1, 4096), (1, 65536), (64, 4096)):
+        cli = CurveBatchEngine(arena_bytes=count * n + (1 << 20))
+        srv = CurveBatchEngine(arena_bytes=1 << 20)
+        cc, sc = cli.add_connection(PRECOM), srv.add_connection(PRECOM, as_server=True)
+        payload = np.random.default_rng(n).integers(0, 256, size=count * n, dtype=np.uint8).tobytes()
+        t_out, t_in, ok = [], [], True
+        for r in range(reps):
+            for k in range(count):
+                buf = cli.msg_alloc(n)
+                ctypes.memmove(buf, payload[k * n:(k + 1) * n], n)
+                cli.send(cc, buf)
+            t0 = time.perf_counter()
+            cli.flush_out()
+            t_out.append(time.perf_counter() - t0)
+            srv.recv(sc, cli.wire_out(cc))
+            t0 = time.perf_counter()
+            srv.flush_in()
+            t_in.append(time.perf_counter() - t0)
+            got = srv.messages_in(sc)
+            ok = ok and len(got) == count and all(got[k][0] == payload[k * n:(k + 1) * n] for k in range(count))
+        rows.append({"messages": count, "payload_bytes": n, "flush_out_us": round(float(np.median(t_out)) * 1e6, 1),
+                     "flush_in_us": round(float(np.median(t_in)) * 1e6, 1), "verified": bool(ok)})
+        del cli, srv
+    return rows
 
 
 def _libsodium():

@@ -44,6 +44,14 @@ namespace {
 constexpr uint64_t SLOT_ALIGN = 128;  // body / payload slots: line-staged stores, whole-line loads
 constexpr uint32_t SEG_BLOCKS = 128;  // as jeromq_amd.batch.SEG_BLOCKS
 
+// Segment length for a flush of `blocks` 64-byte blocks in all: SEG_BLOCKS once there are 64K
+// lanes' worth, shorter below that (down to 4) so that a small flush spreads each frame over many
+// lanes instead of walking it on one (a 4 KiB frame alone: 65 blocks on one lane, ~150 us).
+uint32_t flush_seg_blocks(uint64_t blocks)
+{
+    return (uint32_t)std::min<uint64_t>(SEG_BLOCKS, std::max<uint64_t>(4, (blocks + 65535) / 65536));
+}
+
 uint64_t round_up(uint64_t v, uint64_t a) { return (v + a - 1) / a * a; }
 
 // CZ_ENGINE_TRACE=1: per-phase wall times of each flush on stderr (profiling aid)
@@ -318,6 +326,7 @@ struct cz_engine {
         }
         wpos[n] = w;
         wire_total = w;
+        const uint32_t seg = flush_seg_blocks(w / 64);
         // 2. groups of ~equal wire bytes: [fa, fb) in send order, body slots contiguous per group;
         //    per group the arena prefix it needs, its body-slot base and its segment / combine
         //    counts (plan_counts) -- enough to size every buffer and start the arena copy before
@@ -347,7 +356,7 @@ struct cz_engine {
                 const OutMsg &m = pend[i];
                 slot += round_up((uint64_t)m.len + CZ_MESSAGE_OVERHEAD, SLOT_ALIGN);
                 hi = std::max<uint64_t>(hi, m.arena_off + m.len);
-                plan_counts(m.len, 0, SEG_BLOCKS, ns, nc, np);
+                plan_counts(m.len, 0, seg, ns, nc, np);
             }
             g.arena_hi = hi;
             soff[gi + 1] = soff[gi] + ns;
@@ -380,7 +389,11 @@ struct cz_engine {
             if ((e = hipEventCreateWithFlags(&ev[gi], hipEventDisableTiming)) != hipSuccess ||
                 (e = hipEventCreateWithFlags(&evk[gi], hipEventDisableTiming)) != hipSuccess)
                 return hip_fail(e, "hipEventCreate");
+        // one group: no overlap to gain, so one stream and no cross-stream events (each costs
+        // tens of us, the bulk of a small flush's latency)
         hipStream_t qh = ps[0], qk = ps[1], qo = ps[2];
+        if (groups.size() == 1)
+            qh = qo = qk;
         uint64_t copied = 0;
         // the arena bytes not copied yet up to group g's last payload
         auto copy_arena = [&](size_t gi) -> hipError_t {
@@ -406,7 +419,7 @@ struct cz_engine {
                 h_items[i] = {bs, wpos[i], (uint32_t)body, (uint32_t)CZ_V2_ITEM_HEADER};
                 bs += round_up(body, SLOT_ALIGN);
             }
-            plan_segments(h_desc + g.fa, gn, 0, SEG_BLOCKS, sg.seg, sg.comb, sg.npart);
+            plan_segments(h_desc + g.fa, gn, 0, seg, sg.seg, sg.comb, sg.npart);
             const uint32_t gseg = (uint32_t)sg.seg.size(), gcomb = (uint32_t)sg.comb.size();
             if (gseg != soff[gi + 1] - soff[gi] || gcomb != coff[gi + 1] - coff[gi] || sg.npart != woff[gi + 1] - woff[gi])
                 return fail(CZ_EINVAL, "cz_engine: segment plan disagrees with its count");
@@ -427,17 +440,18 @@ struct cz_engine {
                 (gcomb && (e = hipMemcpyAsync(dcb, (const cz_combine *)(hm + m_comb) + coff[gi],
                                               (uint64_t)gcomb * sizeof(cz_combine), hipMemcpyHostToDevice, qh)) !=
                               hipSuccess) ||
-                (e = hipEventRecord(ev[gi], qh)) != hipSuccess || (e = copy_arena(gi + 1)) != hipSuccess)
+                (qh != qk && (e = hipEventRecord(ev[gi], qh)) != hipSuccess) ||
+                (e = copy_arena(gi + 1)) != hipSuccess)
                 return hip_fail(e, "cz_engine: flush_out H2D");
             // (b) compute stream: seal into body slots, pack behind V2 headers at the send-order
             //     wire positions; (c) D2H stream: the group's wire bytes back
-            if ((e = hipStreamWaitEvent(qk, ev[gi], 0)) != hipSuccess ||
+            if ((qh != qk && (e = hipStreamWaitEvent(qk, ev[gi], 0)) != hipSuccess) ||
                 (e = czk_seal_segments(dd, dsg, gseg, dcb, gcomb, d_in.ptr, d_body.ptr, subkeys.ptr,
                                        (uint8_t *)d_work.ptr + 64 * woff[gi], qk)) != hipSuccess ||
                 (e = czk_v2_copy((const cz_v2_item *)d_items.ptr + g.fa, gn, d_body.ptr, d_wire.ptr, qk)) !=
                     hipSuccess ||
-                (e = hipEventRecord(evk[gi], qk)) != hipSuccess ||
-                (e = hipStreamWaitEvent(qo, evk[gi], 0)) != hipSuccess ||
+                (qo != qk && ((e = hipEventRecord(evk[gi], qk)) != hipSuccess ||
+                              (e = hipStreamWaitEvent(qo, evk[gi], 0)) != hipSuccess)) ||
                 (e = hipMemcpyAsync((uint8_t *)h_wire.ptr + wpos[g.fa], (uint8_t *)d_wire.ptr + wpos[g.fa],
                                     wpos[g.fb] - wpos[g.fa], hipMemcpyDeviceToHost, qo)) != hipSuccess)
                 return hip_fail(e, "cz_engine: flush_out");
@@ -484,6 +498,7 @@ struct cz_engine {
             parsed.push_back({(uint32_t)ci, 0u, 0u, 0u, 0u, 0});
             rx_total += c.rx_len;
         }
+        const uint32_t seg = flush_seg_blocks(rx_total / 64);
         struct Group {
             size_t pa, pb;        // parsed[pa, pb)
             uint32_t fa, fb;      // frames[fa, fb)
@@ -517,6 +532,8 @@ struct cz_engine {
         // each group into one pinned slab on 8 host threads (the memcpy is slower than the gaps it
         // removes) and hipMemcpyBatchAsync of the per-connection copies (the same gaps).)
         hipStream_t qh = ps[0], qk = ps[1], qo = ps[2], qm = stream;
+        if (groups.size() <= 1)  // as flush_out: one group, one stream
+            qh = qo = qm = qk;
         std::vector<hipEvent_t> ev(groups.size(), nullptr);
         EvGuard evguard{ev};
         for (size_t gi = 0; gi < groups.size(); gi++)
@@ -568,7 +585,7 @@ struct cz_engine {
                 if ((e = hipMemcpyAsync((uint8_t *)d_wire.ptr + spans[si].dev, spans[si].src, spans[si].len,
                                         hipMemcpyHostToDevice, qh)) != hipSuccess)
                     return hip_fail(e, "cz_engine: H2D");
-            if ((e = hipEventRecord(ev[gi], qh)) != hipSuccess)
+            if (qh != qk && (e = hipEventRecord(ev[gi], qh)) != hipSuccess)
                 return hip_fail(e, "cz_engine: H2D");
         }
         pt.mark("h2d-issue");
@@ -617,7 +634,7 @@ struct cz_engine {
                 const uint64_t plen = f.size > CZ_MESSAGE_OVERHEAD ? f.size - CZ_MESSAGE_OVERHEAD : 0;
                 w.bslot += round_up(std::max<uint64_t>(f.size, 1), SLOT_ALIGN);
                 w.pslot += round_up(std::max<uint64_t>(plen, 1), SLOT_ALIGN);
-                plan_counts(f.size, 1, SEG_BLOCKS, w.nseg, w.ncomb, w.npart);
+                plan_counts(f.size, 1, seg, w.nseg, w.ncomb, w.npart);
             }
         };
         {
@@ -703,7 +720,7 @@ struct cz_engine {
                 }
             }
             const uint32_t gn = g.fb - g.fa;
-            plan_segments(desc, gn, 1, SEG_BLOCKS, w.sg.seg, w.sg.comb, w.sg.npart);
+            plan_segments(desc, gn, 1, seg, w.sg.seg, w.sg.comb, w.sg.npart);
             w.sg.nseg = (uint32_t)w.sg.seg.size();
             w.sg.ncomb = (uint32_t)w.sg.comb.size();
             if (w.sg.nseg != w.nseg || w.sg.ncomb != w.ncomb || w.sg.npart != w.npart) {
@@ -732,17 +749,18 @@ struct cz_engine {
                                                   hipMemcpyHostToDevice, qm)) != hipSuccess) ||
                 (w.sg.ncomb && (r = hipMemcpyAsync(dcb, h_comb + w.coff, (uint64_t)w.sg.ncomb * sizeof(cz_combine),
                                                    hipMemcpyHostToDevice, qm)) != hipSuccess) ||
-                (r = hipEventRecord(evm[gi], qm)) != hipSuccess)
+                (qm != qk && (r = hipEventRecord(evm[gi], qm)) != hipSuccess))
                 return r;
             // (b) compute stream: once the group's bytes and metadata landed, unpack + open;
             // (c) D2H stream
-            if ((r = hipStreamWaitEvent(qk, ev[gi], 0)) != hipSuccess ||
-                (r = hipStreamWaitEvent(qk, evm[gi], 0)) != hipSuccess ||
+            if ((qh != qk && (r = hipStreamWaitEvent(qk, ev[gi], 0)) != hipSuccess) ||
+                (qm != qk && (r = hipStreamWaitEvent(qk, evm[gi], 0)) != hipSuccess) ||
                 (r = czk_v2_copy((const cz_v2_item *)d_items.ptr + g.fa, gn, d_wire.ptr, d_in.ptr, qk)) != hipSuccess ||
                 (r = czk_open_segments(dd, dsg, w.sg.nseg, dcb, w.sg.ncomb, d_in.ptr, d_plain.ptr, subkeys.ptr,
                                        (uint8_t *)d_work.ptr + 64 * w.woff, (uint16_t *)d_status.ptr + g.fa,
                                        (uint64_t *)d_nonces.ptr + g.fa, qk)) != hipSuccess ||
-                (r = hipEventRecord(evk[gi], qk)) != hipSuccess || (r = hipStreamWaitEvent(qo, evk[gi], 0)) != hipSuccess ||
+                (qo != qk && ((r = hipEventRecord(evk[gi], qk)) != hipSuccess ||
+                              (r = hipStreamWaitEvent(qo, evk[gi], 0)) != hipSuccess)) ||
                 (r = hipMemcpyAsync((uint8_t *)h_plain.ptr + g.pl0, (uint8_t *)d_plain.ptr + g.pl0, g.pl1 - g.pl0,
                                     hipMemcpyDeviceToHost, qo)) != hipSuccess ||
                 (r = hipMemcpyAsync((uint16_t *)h_status.ptr + g.fa, (uint16_t *)d_status.ptr + g.fa, (uint64_t)gn * 2,
@@ -771,8 +789,9 @@ struct cz_engine {
             if (e != hipSuccess)
                 return hip_fail(e, "cz_engine: flush_in");
         }
-        for (hipStream_t q : {qh, qk, qo, qm})
-            if ((e = hipStreamSynchronize(q)) != hipSuccess)
+        const hipStream_t used[4] = {qh, qk, qo, qm};
+        for (int i = 0; i < 4; i++)
+            if (std::find(used, used + i, used[i]) == used + i && (e = hipStreamSynchronize(used[i])) != hipSuccess)
                 return hip_fail(e, "cz_engine: flush_in");
         pt.mark("h2d+kernels+d2h");
         // 3. deliver in order per connection, up to the first failure (decodeAndPush returns false)

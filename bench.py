@@ -582,6 +582,23 @@ def nacl_latency(args, dev):
             t_s = med(lambda: sod.crypto_box_afternm(cs, m, ctypes.c_ulonglong(mlen), nonce, k), 2000)
             row["libsodium_1core_us"] = round(t_s * 1e6, 2)
         rows.append(row)
+    # the Mechanism mirror (cz_mech_encode / decode), one MESSAGE per call
+    from jeromq_amd.mechanism import CurveClientMechanism, CurveServerMechanism, Msg
+    mrows = []
+    for n in (100, 4096, 65536, 262144):
+        cli, srv = CurveClientMechanism(PRECOM), CurveServerMechanism(PRECOM)
+        msg = Msg(np.random.default_rng(n).integers(0, 256, size=n, dtype=np.uint8).tobytes())
+        t_enc, t_dec, ok = [], [], True
+        for _ in range(100):
+            t0 = time.perf_counter()
+            enc = cli.encode(msg)
+            t_enc.append(time.perf_counter() - t0)
+            t0 = time.perf_counter()
+            dec = srv.decode(enc)
+            t_dec.append(time.perf_counter() - t0)
+            ok = ok and dec is not None and dec.data == msg.data
+        mrows.append({"payload_bytes": n, "encode_us": round(float(np.median(t_enc)) * 1e6, 1),
+                      "decode_us": round(float(np.median(t_dec)) * 1e6, 1), "verified": bool(ok)})
     # batched host-staged API at 4 KiB: per-call time for B messages
     ctx = ctypes.c_void_p()
     _lib.check(lib.cz_ctx_create(ctypes.byref(ctx), dev.index or 0), "cz_ctx_create")
@@ -602,7 +619,8 @@ def nacl_latency(args, dev):
     win = next((b["batch"] for b in batches if b["per_msg_us"] < ref_us), None)
     return {"metric": "jnacl drop-in single-message latency (cz_box_afternm / open), host buffers",
             "value": rows[1]["seal_us"], "unit": "us per 4 KiB message", "higher_is_better": False, "n_gpus": 1,
-            "ctypes_call_overhead_us": round(t_ctypes * 1e6, 2), "single_shot": rows, "batched_4k": batches,
+            "ctypes_call_overhead_us": round(t_ctypes * 1e6, 2), "single_shot": rows, "mechanism_single": mrows,
+            "batched_4k": batches,
             "batch_beating_one_cpu_core": win,
             "cpu_reference_for_crossover": "libsodium crypto_box_afternm, 1 core" if sod is not None else "oracle, 1 core"}
 

@@ -44,9 +44,11 @@ namespace {
 constexpr uint64_t SLOT_ALIGN = 128;  // body / payload slots: line-staged stores, whole-line loads
 constexpr uint32_t SEG_BLOCKS = 128;  // as jeromq_amd.batch.SEG_BLOCKS
 
-// Segment length for a flush of `blocks` 64-byte blocks in all: SEG_BLOCKS once there are 64K
-// lanes' worth, shorter below that (down to 4) so that a small flush spreads each frame over many
-// lanes instead of walking it on one (a 4 KiB frame alone: 65 blocks on one lane, ~150 us).
+// Segment length for a received flush of `blocks` 64-byte blocks in all (frame sizes are known
+// only after the parse): SEG_BLOCKS once there are 64K lanes' worth, shorter below that (down to
+// 4) so that a small flush spreads each frame over many lanes instead of walking it on one (a
+// 4 KiB frame alone: 65 blocks on one lane, ~150 us).  flush_out knows its lengths up front and
+// uses batch_seg_blocks.
 uint32_t flush_seg_blocks(uint64_t blocks)
 {
     return (uint32_t)std::min<uint64_t>(SEG_BLOCKS, std::max<uint64_t>(4, (blocks + 65535) / 65536));
@@ -311,11 +313,12 @@ struct cz_engine {
         }
         // 1. send-order wire positions and each connection's runs
         std::vector<uint64_t> wpos(n + 1);
-        uint64_t w = 0;
+        uint64_t w = 0, longest = 0;
         for (uint32_t i = 0; i < n; i++) {
             const OutMsg &m = pend[i];
             Conn &c = conns[m.conn];
             const uint64_t body = (uint64_t)m.len + CZ_MESSAGE_OVERHEAD;
+            longest = std::max<uint64_t>(longest, body);
             const uint64_t fb = cz_v2_header_size(body) + body;
             wpos[i] = w;
             if (!c.runs.empty() && c.runs.back().off + c.runs.back().len == w)
@@ -326,7 +329,7 @@ struct cz_engine {
         }
         wpos[n] = w;
         wire_total = w;
-        const uint32_t seg = flush_seg_blocks(w / 64);
+        const uint32_t seg = batch_seg_blocks(w / 64, (longest + 63) / 64);
         // 2. groups of ~equal wire bytes: [fa, fb) in send order, body slots contiguous per group;
         //    per group the arena prefix it needs, its body-slot base and its segment / combine
         //    counts (plan_counts) -- enough to size every buffer and start the arena copy before

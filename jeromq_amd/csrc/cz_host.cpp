@@ -27,8 +27,6 @@ hipError_t czk_open_desc(const cz_frame_desc *, const uint32_t *, uint32_t, cons
 hipError_t czk_open_uniform(const void *, uint64_t, void *, uint64_t, uint32_t, uint32_t, const void *, uint64_t, int,
                             uint16_t *, hipStream_t);
 hipError_t czk_box_nacl(const void *, void *, uint32_t, const void *, uint64_t, int, int *, hipStream_t);
-hipError_t czk_nacl_one(void *, uint32_t, int, void *, int, uint32_t, const uint8_t *, const uint8_t *, hipStream_t);
-uint32_t czk_nacl_one_max(void);
 hipError_t czk_fill(void *, uint64_t, uint64_t, hipStream_t);
 hipError_t czk_copy16(void *, const void *, uint64_t, hipStream_t);
 int czk_tune(const char *, int);
@@ -157,17 +155,6 @@ static int single_init()
 }
 
 static uint64_t up128(uint64_t v) { return (v + 127) & ~127ull; }
-
-// segment length for one message of nblk blocks: a lane walks seg + 1 blocks (block 0 gives its
-// Poly1305 key) and the combine lane walks the nblk / seg segments serially, so the latency is
-// ~ (seg + 1) * T_block + (nblk / seg) * T_combine, T_block / T_combine ~ 18
-static uint32_t single_seg_blocks(uint32_t nblk)
-{
-    uint32_t s = 2;
-    while ((s + 1) * (s + 1) * 18 <= nblk)
-        s++;
-    return s;
-}
 
 // NaCl box/open of one message in ONE launch (k_nacl_one): input staged into pinned host memory
 // the kernel reads directly, output read back from it after the launch.  -1 on a bad tag (dst
@@ -855,8 +842,7 @@ static int ctx_uniform_segments(cz_ctx *c, bool seal, uint32_t count, uint32_t l
         in_stride = len;
         out_stride = std::max<uint64_t>(olen, 1);
     }
-    uint32_t seg = std::max<uint32_t>(single_seg_blocks(nblk), (uint32_t)(((uint64_t)count * nblk + 65535) / 65536));
-    seg = std::min<uint32_t>(seg, 128);
+    const uint32_t seg = batch_seg_blocks((uint64_t)count * nblk, nblk);
     const uint32_t lead = seal ? 0u : 1u;
     const bool split = nblk > seg + seg / 2;
     const uint32_t ns = split ? (nblk - lead + seg - 1) / seg : 1u;

@@ -19,6 +19,8 @@ hipError_t czk_seal_segments(const cz_frame_desc *, const cz_segment *, uint32_t
 hipError_t czk_open_segments(const cz_frame_desc *, const cz_segment *, uint32_t, const cz_combine *, uint32_t,
                              const void *, void *, const void *, void *, uint16_t *, uint64_t *, hipStream_t);
 hipError_t czk_v2_copy(const cz_v2_item *, uint32_t, const void *, void *, hipStream_t);
+hipError_t czk_nacl_one(void *, uint32_t, int, void *, int, uint32_t, const uint8_t *, const uint8_t *, hipStream_t);
+uint32_t czk_nacl_one_max(void);
 }
 
 namespace czi {
@@ -46,6 +48,28 @@ inline void plan_counts(uint64_t len, int open, uint32_t seg_blocks, uint64_t &n
     nseg += ns;
     npart += ns;
     ncomb += 1;
+}
+
+// Segment length for ONE frame of nblk blocks on its own: a lane walks seg + 1 blocks (block 0
+// gives its Poly1305 key) and the combine lane walks the nblk / seg segments serially, so the
+// latency is ~ (seg + 1) * T_block + (nblk / seg) * T_combine, T_block / T_combine ~ 18
+// (DESIGN.md section 4).
+inline uint32_t single_seg_blocks(uint64_t nblk)
+{
+    uint32_t s = 2;
+    while ((uint64_t)(s + 1) * (s + 1) * 18 <= nblk)
+        s++;
+    return s;
+}
+
+// Segment length for a batch of `total` blocks whose longest frame has `longest` blocks: 128
+// (SEG_BLOCKS, the throughput setting) once the batch has 64K lanes' worth, shorter below that, so
+// a small batch spreads its frames over many lanes; never shorter than the one-frame optimum.
+inline uint32_t batch_seg_blocks(uint64_t total, uint64_t longest)
+{
+    uint64_t s = (total + 65535) / 65536;
+    s = s > single_seg_blocks(longest) ? s : single_seg_blocks(longest);
+    return (uint32_t)(s < 128 ? s : 128);
 }
 
 // device buffer that grows on demand (never shrinks)

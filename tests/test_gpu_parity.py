@@ -515,6 +515,46 @@ def test_mechanism_batches(L, torch_dev):
     assert srv.last_event == L.CZ_ZMTP_CRYPTOGRAPHIC
 
 
+def test_mechanism_one_launch_and_segmented_paths(L, torch_dev):
+    """encode / decode of one MESSAGE up to 80 KiB run in one launch (k_nacl_one) with the
+    mechanism's own subkeys; longer ones and batches run the segment kernels with the segment length
+    scaled to the batch.  Bodies against the oracle on both sides of the 80 KiB edge, a ragged batch
+    of long and short frames, and the header rejections of the one-launch path (short body,
+    wrong command, replay) against the reference's events."""
+    from jeromq_amd.mechanism import CurveClientMechanism, CurveServerMechanism, Msg
+    cli = CurveClientMechanism(PRECOM)
+    srv = CurveServerMechanism(PRECOM)
+    nonce = 3
+    for n in (81919 - 33, 81920 - 33, 81921 - 33, 200000):
+        p = splitmix_bytes(n, n)
+        enc = cli.encode(Msg(p, 1))
+        assert enc.data == or_curve_encode(p, 1, nonce, 0, PRECOM), n
+        dec = srv.decode(enc)
+        assert dec is not None and dec.data == p and dec.flags == 1, n
+        nonce += 1
+    msgs = [Msg(splitmix_bytes(n, 7 * n + 1), n & 3) for n in (100000, 1, 5000, 0, 300000, 64)]
+    enc = cli.encodeBatch(msgs)
+    for i, (m, e) in enumerate(zip(msgs, enc)):
+        assert e.data == or_curve_encode(m.data, m.flags, nonce + i, 0, PRECOM), i
+    dec = srv.decodeBatch(enc)
+    assert [d.data for d in dec] == [m.data for m in msgs] and [d.flags for d in dec] == [m.flags for m in msgs]
+    assert srv.cnPeerNonce == nonce + len(msgs) - 1
+    # one-launch decode rejections: nothing changes but the event (and cnPeerNonce on a bad tag)
+    before = srv.cnPeerNonce
+    assert srv.decode(Msg(b"\x07MESS")) is None and srv.last_event == L.CZ_ZMTP_UNEXPECTED_COMMAND
+    assert srv.decode(enc[-1]) is None and srv.last_event == L.CZ_ZMTP_INVALID_SEQUENCE
+    assert srv.cnPeerNonce == before
+    fresh = bytearray(cli.encode(Msg(b"tampered")).data)
+    fresh[20] ^= 0x40                                        # the tag
+    assert srv.decode(Msg(bytes(fresh))) is None and srv.last_event == L.CZ_ZMTP_CRYPTOGRAPHIC
+    assert srv.cnPeerNonce == before + 1                     # set before the tag check (:193)
+    # byte 7 of the command name is not compared (Msgs.java:31), as the kernels do
+    odd = bytearray(cli.encode(Msg(b"ok", 2)).data)
+    odd[7] ^= 0x55
+    got = srv.decode(Msg(bytes(odd)))
+    assert got is not None and got.data == b"ok" and got.flags == 2
+
+
 def test_ctx_host_staged(L, torch_dev):
     lib = L.lib()
     ctx = ctypes.c_void_p()

@@ -784,24 +784,46 @@ static int ctx_run(cz_ctx *c, const cz_frame_desc *h_desc, uint32_t count, const
         return rc;
     if (count == 0)
         return CZ_OK;
+    // segment kernels, the segment length scaled to the batch (batch_seg_blocks): a batch of a few
+    // long frames spreads over many lanes instead of walking each frame on one
+    uint64_t tb = 0, longest = 0;
+    for (uint32_t i = 0; i < count; i++) {
+        const uint64_t nb = ((seal ? (uint64_t)h_desc[i].len + CZ_MESSAGE_OVERHEAD : (uint64_t)h_desc[i].len) + 63) / 64;
+        tb += nb;
+        longest = std::max<uint64_t>(longest, nb);
+    }
+    std::vector<cz_segment> segs;
+    std::vector<cz_combine> combs;
+    uint32_t npart = 0;
+    plan_segments(h_desc, count, seal ? 0 : 1, batch_seg_blocks(tb, longest), segs, combs, npart);
+    const uint64_t m_seg = sizeof(cz_frame_desc) * (uint64_t)count, m_comb = m_seg + sizeof(cz_segment) * segs.size(),
+                   m_end = m_comb + sizeof(cz_combine) * combs.size();
     hipError_t e;
     (void)hipSetDevice(c->device);
-    if ((e = c->desc.reserve(sizeof(cz_frame_desc) * (uint64_t)count)) != hipSuccess ||
+    if ((e = c->desc.reserve(m_end)) != hipSuccess || (e = c->hdesc.reserve(m_end)) != hipSuccess ||
         (e = c->in.reserve(in_bytes + 16)) != hipSuccess || (e = c->out.reserve(out_bytes + 16)) != hipSuccess ||
-        (e = c->status.reserve(sizeof(uint16_t) * (uint64_t)count)) != hipSuccess)
+        (e = c->status.reserve(sizeof(uint16_t) * (uint64_t)count)) != hipSuccess ||
+        (e = c->work.reserve(64ull * std::max<uint32_t>(npart, 1))) != hipSuccess)
         return hip_fail(e, "hipMalloc");
-    if ((e = hipMemcpyAsync(c->desc.ptr, h_desc, sizeof(cz_frame_desc) * (uint64_t)count, hipMemcpyHostToDevice,
-                            c->stream)) != hipSuccess ||
+    uint8_t *hm = (uint8_t *)c->hdesc.ptr;
+    memcpy(hm, h_desc, m_seg);
+    memcpy(hm + m_seg, segs.data(), m_comb - m_seg);
+    memcpy(hm + m_comb, combs.data(), m_end - m_comb);
+    const uint8_t *dm = (const uint8_t *)c->desc.ptr;
+    if ((e = hipMemcpyAsync(c->desc.ptr, hm, m_end, hipMemcpyHostToDevice, c->stream)) != hipSuccess ||
         (e = hipMemcpyAsync(c->in.ptr, h_in, in_bytes, hipMemcpyHostToDevice, c->stream)) != hipSuccess)
         return hip_fail(e, "H2D");
+    const cz_frame_desc *dd = (const cz_frame_desc *)dm;
+    const cz_segment *ds = (const cz_segment *)(dm + m_seg);
+    const cz_combine *dc = (const cz_combine *)(dm + m_comb);
     if (seal) {
-        e = czk_seal_desc((const cz_frame_desc *)c->desc.ptr, nullptr, count, c->in.ptr, c->out.ptr, c->subkeys.ptr,
-                          c->stream);
+        e = czk_seal_segments(dd, ds, (uint32_t)segs.size(), dc, (uint32_t)combs.size(), c->in.ptr, c->out.ptr,
+                              c->subkeys.ptr, c->work.ptr, c->stream);
     } else {
         if (out_bytes && (e = hipMemsetAsync(c->out.ptr, 0, out_bytes, c->stream)) != hipSuccess)
             return hip_fail(e, "memset");
-        e = czk_open_desc((const cz_frame_desc *)c->desc.ptr, nullptr, count, c->in.ptr, c->out.ptr, c->subkeys.ptr,
-                          (uint16_t *)c->status.ptr, nullptr, c->stream);
+        e = czk_open_segments(dd, ds, (uint32_t)segs.size(), dc, (uint32_t)combs.size(), c->in.ptr, c->out.ptr,
+                              c->subkeys.ptr, c->work.ptr, (uint16_t *)c->status.ptr, nullptr, c->stream);
     }
     if (e != hipSuccess)
         return hip_fail(e, "launch");

@@ -561,7 +561,8 @@ def test_ctx_host_staged(L, torch_dev):
     L.check(lib.cz_ctx_create(ctypes.byref(ctx), 0))
     try:
         L.check(lib.cz_ctx_set_keys(ctx, PRECOM, 1, L.CZ_DIR_S2C))
-        frames = [(splitmix_bytes(n, 3 * n), 1, 2 + i, 0) for i, n in enumerate([0, 10, 100, 1000, 5000])]
+        sizes = [0, 10, 100, 1000, 5000, 200000, 70000, 64]
+        frames = [(splitmix_bytes(n, 3 * n), 1, 2 + i, 0) for i, n in enumerate(sizes)]
         desc, hin, ob = _pack(frames)
         hout = np.zeros(ob, dtype=np.uint8)
         L.check(lib.cz_ctx_seal(ctx, desc.ctypes.data, len(desc), hin.ctypes.data, hin.nbytes, hout.ctypes.data,
@@ -569,6 +570,28 @@ def test_ctx_host_staged(L, torch_dev):
         for i, (p, fl, ctr, k) in enumerate(frames):
             o = int(desc[i]["out_off"])
             assert hout[o:o + len(p) + 33].tobytes() == or_curve_encode(p, fl, ctr, 1, PRECOM)
+        # cz_ctx_open of the same bodies: nonce floors chained through prev, a bad tag in frame 5
+        # (200 KB: several segments, the combine kernel's reject) and a replay in frame 7
+        bodies = [hout[int(d["out_off"]):int(d["out_off"]) + int(d["len"]) + 33].tobytes() for d in desc]
+        bodies[5] = bodies[5][:100] + bytes([bodies[5][100] ^ 1]) + bodies[5][101:]
+        bodies[7] = bodies[7][:8] + bodies[6][8:16] + bodies[7][16:]
+        odesc, obody, pb = _pack([(b, 0, 0, 0) for b in bodies], overhead=-33)
+        odesc["counter"] = 1
+        odesc["flags"] = L.CZ_DESC_CHECK_NONCE
+        odesc["prev"] = np.arange(len(bodies)) - 1
+        plain = np.full(pb, 0xEE, dtype=np.uint8)
+        st = np.full(len(bodies), 0xFFFF, dtype=np.uint16)
+        L.check(lib.cz_ctx_open(ctx, odesc.ctypes.data, len(odesc), obody.ctypes.data, obody.nbytes,
+                                plain.ctypes.data, plain.nbytes, st.ctypes.data))
+        want = [L.CZ_STATUS_OK] * len(bodies)
+        want[5], want[7] = L.CZ_STATUS_CRYPTO, L.CZ_STATUS_SEQUENCE
+        assert list(st & 0xff) == want
+        for i, (p, fl, _c, _k) in enumerate(frames):
+            o = int(odesc[i]["out_off"])
+            if want[i] == L.CZ_STATUS_OK:
+                assert plain[o:o + len(p)].tobytes() == p and st[i] >> 8 == fl, i
+            else:
+                assert not plain[o:o + len(p)].any(), i
         # out-of-bounds descriptor is rejected before any launch
         bad = desc.copy()
         bad["in_off"][0] = hin.nbytes

@@ -327,3 +327,34 @@ def test_engine_fuzz_roundtrip(torch_dev, L, seed):
         assert got[i] == sent[i], f"connection {i}"
         if sent[i]:
             assert srv.peer_nonce(sc[i]) == 3 + len(sent[i]) - 1
+
+
+def test_engine_full_size_flush(torch_dev, L):
+    """bench.py's engine line at full size: 1024 connections x 256 x 4 KiB (1 GiB per flush, 16
+    pipelined groups, 128-block segments).  32 connections' whole wire streams against the oracle,
+    and every one of the 262144 messages delivered intact by the server engine's flush_in."""
+    from jeromq_amd.engine import CurveBatchEngine
+    nconn, per, n = 1024, 256, 4096
+    cli = CurveBatchEngine(arena_bytes=nconn * per * n + (1 << 20))
+    srv = CurveBatchEngine(arena_bytes=1 << 20)
+    cc = [cli.add_connection(_precom(c)) for c in range(nconn)]
+    sc = [srv.add_connection(_precom(c), as_server=True) for c in range(nconn)]
+    payload = np.frombuffer(splitmix_bytes(per * n + 64 * nconn, 77), dtype=np.uint8)
+    for c in range(nconn):                     # each connection's messages: a window shifted by 64 c
+        for k in range(per):
+            buf = cli.msg_alloc(n)
+            ctypes.memmove(buf, payload[64 * c + k * n:64 * c + (k + 1) * n].ctypes.data, n)
+            cli.send(cc[c], buf, more=(k % 8 == 0))
+    cli.flush_out()
+    for c in list(range(0, nconn, 37)) + [nconn - 1]:
+        msgs = [(payload[64 * c + k * n:64 * c + (k + 1) * n].tobytes(), int(k % 8 == 0)) for k in range(per)]
+        assert cli.wire_out(cc[c]) == _oracle_wire(msgs, _precom(c), 0, 3), f"connection {c}"
+    for c in range(nconn):
+        srv.recv(sc[c], cli.wire_out(cc[c]))
+    srv.flush_in()
+    for c in range(nconn):
+        got = srv.messages_in(sc[c])
+        assert len(got) == per and srv.error(sc[c]) == (0, 0), c
+        for k in range(per):
+            assert got[k][0] == payload[64 * c + k * n:64 * c + (k + 1) * n].tobytes(), (c, k)
+        assert srv.peer_nonce(sc[c]) == 3 + per - 1

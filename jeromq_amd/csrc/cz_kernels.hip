@@ -120,6 +120,28 @@ typedef __attribute__((address_space(1))) u16_ua g_u16_ua;
 typedef v4u_t v4u_ua __attribute__((aligned(1)));
 typedef __attribute__((address_space(1))) v4u_ua g_v4u_ua;
 
+// 16-byte line store through a buffer resource: `base` wave-uniform (SGPRs), `voff` this lane's
+// 32-bit offset, soffset the constant 0.  Never give these stores a REGISTER soffset: LLVM's
+// hazard recognizer assumes a MUBUF store with a register soffset has no store-data hazard and
+// lets the next VALU rewrite the data VGPRs right behind the store, and on gfx950 the store then
+// writes the new value (round 3: one dword per 16 bytes replaced by an LDS address, a few lines
+// per 2^20-frame Zipf batch).  With soffset 0 it inserts the wait state, and
+// tests/test_isa_hazards.py checks the listing for any MUBUF store with a register soffset.
+__device__ __forceinline__ void buf_store16(u64 base, u32 voff, uint4 v)
+{
+    const __amdgpu_buffer_rsrc_t rs =
+        __builtin_amdgcn_make_buffer_rsrc(reinterpret_cast<void *>((uintptr_t)base), 0, (int)0xffffffffu, 0x00020000);
+    __builtin_amdgcn_raw_buffer_store_b128(v4u_t{v.x, v.y, v.z, v.w}, rs, (int)voff, 0, 0);
+}
+
+// wave-uniform copy of a 64-bit value (each half through u32: readfirstlane returns int, and a low
+// half with bit 31 set would sign-extend over the high one)
+__device__ __forceinline__ u64 uniform64(u64 v)
+{
+    return ((u64)(u32)__builtin_amdgcn_readfirstlane((u32)(v >> 32)) << 32) |
+           (u64)(u32)__builtin_amdgcn_readfirstlane((u32)v);
+}
+
 // store bytes [a, b) (0 <= a <= b <= 16) of the unit v whose byte 0 belongs at p
 __device__ void st_range16(uint8_t *p, uint4 v, u32 a, u32 b)
 {
@@ -331,22 +353,15 @@ struct EmitLines {
         uint8_t *p = wbase + 128u * r + 16u * c;  // every line of the wave onto its first 8 KiB
         const u64 step = 1024u;  // (diagnostic build: plain stores)
 #else
-        // A buffer store: the line's wave-uniform base in the resource (SGPRs, rebuilt by the
-        // scalar unit per line), this lane's 32-bit offset in a VGPR computed once, and the
-        // j-th frame group's offset j * 8 * stride as the SGPR soffset -- no VALU address
-        // arithmetic at all per store (plain C stores cost a v_lshl_add_u64 each, +8 VALU and
-        // 16 VGPRs per block pair).  It is a compiler builtin, not inline asm, so the backend
-        // counts the store's wait states itself (round 2's asm store was outside its hazard
-        // recognizer, and a rescheduled Poly1305 v_mad_u64_u32 rewrote one store's data VGPRs
-        // one state after issue: DESIGN.md section 6).  The launcher keeps 64 * stride < 2^31.
-        const u64 wb = (u64)(uintptr_t)wbase;
-        // (readfirstlane returns int: each half goes through u32 before widening, or a low half
-        // with bit 31 set would sign-extend over the high one)
-        const u64 lb = (((u64)(u32)__builtin_amdgcn_readfirstlane((u32)(wb >> 32)) << 32) |
-                        (u64)(u32)__builtin_amdgcn_readfirstlane((u32)wb)) +
-                       128ull * line;
-        const __amdgpu_buffer_rsrc_t rs =
-            __builtin_amdgcn_make_buffer_rsrc(reinterpret_cast<void *>((uintptr_t)lb), 0, (int)0xffffffffu, 0x00020000);
+        // A buffer store (buf_store16): the j-th frame group's line base lb + j * 8 * stride in
+        // the resource (SGPRs, advanced by the scalar unit), this lane's 32-bit offset in a VGPR
+        // computed once -- no VALU address arithmetic at all per store (plain C stores cost a
+        // v_lshl_add_u64 each, +8 VALU and 16 VGPRs per block pair).  It is a compiler builtin,
+        // not inline asm, so the backend counts the store's wait states itself (round 2's asm
+        // store was outside its hazard recognizer, and a rescheduled Poly1305 v_mad_u64_u32
+        // rewrote one store's data VGPRs one state after issue: DESIGN.md section 6).  The
+        // launcher keeps 64 * stride < 2^31.
+        const u64 lb = uniform64((u64)(uintptr_t)wbase) + 128ull * line;
         const u32 voff = r * (u32)stride + 16u * c;
         const u32 step = 8u * (u32)stride;
 #endif
@@ -373,7 +388,7 @@ struct EmitLines {
             }
             p += step;
 #else
-                __builtin_amdgcn_raw_buffer_store_b128(v4u_t{v.x, v.y, v.z, v.w}, rs, (int)voff, (int)(j * step), 0);
+                buf_store16(lb + (u64)(j * step), voff, v);
 #endif
         }
     }
@@ -1241,7 +1256,29 @@ constexpr u32 SHEAD = 16;  // row bytes before line-space byte 0 (a chunk's firs
 // workgroup-relative frame index of the 8 outputs it stores for (ds_bpermute) and keeps their
 // 128-byte line offsets from the workgroup's line-aligned base in 8 VGPRs, so the interior-line
 // flush -- the hot one -- is 8 ds_read_b128 + 8 buffer stores with no per-store ds_bpermute and
-// no VALU address arithmetic (the base lives in the SGPR resource, the line in soffset).
+// no VALU address arithmetic (the base lives in the SGPR resource, the line added to it by the scalar unit).
+// The outputs of a wave of ragged segments as 32-bit offsets from one wave-uniform base, so that
+// a line store is a buffer store (base + line in the SGPR resource) fed by one
+// ds_bpermute of the owner's offset.  base = lane 0's output rounded down to 128, minus 2^30;
+// ok when every output lies within [base, base + 2^31) -- the planner's stable sort keeps a
+// wave's segments within a few MiB of each other, so the fallback (64-bit bases) is for
+// far-apart caller buffers only.
+struct WaveRel {
+    u64 base;
+    u32 rel;  // this lane's output - base
+    bool ok;  // wave-uniform
+    __device__ __forceinline__ void init(const uint8_t *mine)
+    {
+        const u64 a = (u64)(uintptr_t)mine;
+        const u64 a0 = uniform64(a);
+        base = (a0 & ~(u64)127) - (1ull << 30);
+        const u64 d = a - base;
+        const bool mine_ok = a0 >= (1ull << 30) + 128u && d < (1ull << 31);
+        ok = __builtin_amdgcn_ballot_w64(!mine_ok) == 0;
+        rel = (u32)d;
+    }
+};
+
 template <bool UNI>
 struct EmitShiftLinesT {
     static constexpr bool cooperative = true;
@@ -1254,6 +1291,7 @@ struct EmitShiftLinesT {
     u32 walign;      // largest of 16 / 8 / 1 that divides every output's line offset in the wave
     u64 ubase;       // UNI: the workgroup's first output address rounded down to 128 (wave-uniform)
     u32 loff[8];     // UNI: line offset from ubase of output F = 8j + lane / 8, plus 16 * (lane & 7)
+    WaveRel wr;      // !UNI: 32-bit output offsets for the interior-line flush
 
     // UNI: rel = this lane's workgroup-relative frame index, wg_out = the workgroup's frame-0 output
     // (the launcher keeps 256 * stride + the output length below 2^31)
@@ -1283,6 +1321,10 @@ struct EmitShiftLinesT {
         te = (d + total) | (tag_slot ? 0x80000000u : 0u);
         const uint64_t a = __builtin_amdgcn_ballot_w64((((u32)(uintptr_t)mine) & 64u) != 0u);
         mixed = (a != 0 && ~a != 0) ? 1u : 0u;
+        if constexpr (!UNI)
+            wr.init(mine);
+        else
+            wr.ok = false;
     }
     // store, for every output F of the wave whose line completes now, its line k_F:
     // KIND FL_PHASE: a one-class wave after chunk q of its phase, every F's line k = q / 2;
@@ -1303,17 +1345,28 @@ struct EmitShiftLinesT {
             const bool inner = k >= 2u && 128u * (k + 1u) <= (te & 0x7fffffffu);
             if constexpr (UNI) {
                 if (__builtin_amdgcn_ballot_w64(!inner) == 0) {
-                    const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(
-                        reinterpret_cast<void *>((uintptr_t)ubase), 0, (int)0xffffffffu, 0x00020000);
-                    const u32 so = (u32)__builtin_amdgcn_readfirstlane(128u * k);
+                    const u64 lb = ubase + (u32)__builtin_amdgcn_readfirstlane(128u * k);
 #pragma unroll
                     for (u32 j = 0; j < 8; j++) {
                         const u32 F = 8u * j + r;
                         const uint4 v = *reinterpret_cast<const uint4 *>(rows + F * SROW + SHEAD + 16u * c);
-                        __builtin_amdgcn_raw_buffer_store_b128(v4u_t{v.x, v.y, v.z, v.w}, rs, (int)loff[j], (int)so, 0);
+                        buf_store16(lb, loff[j], v);
                     }
                     return;
                 }
+            }
+            if (!UNI && wr.ok && __builtin_amdgcn_ballot_w64(!inner) == 0) {
+                // as UNI, with each output's line offset fetched per store (one ds_bpermute + one
+                // VALU instead of two ds_bpermutes and a 64-bit add)
+                const u64 lb = wr.base + (u32)__builtin_amdgcn_readfirstlane(128u * k);
+#pragma unroll
+                for (u32 j = 0; j < 8; j++) {
+                    const u32 F = 8u * j + r;
+                    const uint4 v = *reinterpret_cast<const uint4 *>(rows + F * SROW + SHEAD + 16u * c);
+                    const u32 lo = (u32)__builtin_amdgcn_ds_bpermute((int)(F << 2), (int)wr.rel);
+                    buf_store16(lb, (lo & ~127u) | (16u * c), v);
+                }
+                return;
             }
             if (!UNI && __builtin_amdgcn_ballot_w64(!inner) == 0) {
 #pragma unroll
@@ -1461,8 +1514,13 @@ struct EmitSegLines {
     uint8_t *mine;
     u32 lane, total, last_q;
     u32 tt;          // total | bit 31: leave bytes 16..31 of line 0 to tag()
+    WaveRel wr;      // every output of the wave within 2^30 bytes of lane 0's: 32-bit offsets
 
-    __device__ __forceinline__ void init(bool tag_slot) { tt = total | (tag_slot ? 0x80000000u : 0u); }
+    __device__ __forceinline__ void init(bool tag_slot)
+    {
+        tt = total | (tag_slot ? 0x80000000u : 0u);
+        wr.init(mine);
+    }
     __device__ __forceinline__ void flush(u32 line)
     {
         const u32 c = lane & 7u;
@@ -1470,6 +1528,21 @@ struct EmitSegLines {
         const u32 off = 128u * line + 16u * c;
         const u64 mb = (u64)(uintptr_t)mine;
         asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        // Interior line of every segment in the wave (whole, no tag bytes): one ds_bpermute of the
+        // owner's 32-bit offset and one add per store, base + line in the buffer resource (the
+        // general path below fetches a 64-bit base and a count per store and
+        // clips: ~12 VALU and a branch per store).
+        const bool inner = 128u * line + 128u <= total && !((tt >> 31) && line == 0u);
+        if (wr.ok && __builtin_amdgcn_ballot_w64(!inner) == 0) {
+            const u64 lb = wr.base + (u32)__builtin_amdgcn_readfirstlane(128u * line);
+#pragma unroll
+            for (u32 j = 0; j < 8; j++) {
+                const u32 F = 8u * j + r;
+                const uint4 v = lds[F * 8u + (c ^ (F & 7u))];
+                buf_store16(lb, (u32)__builtin_amdgcn_ds_bpermute((int)(F << 2), (int)wr.rel) + 16u * c, v);
+            }
+            return;
+        }
 #pragma unroll
         for (u32 j = 0; j < 8; j++) {
             const u32 F = 8u * j + r;

@@ -238,6 +238,23 @@ __device__ __forceinline__ V4 ld16f(const uint8_t *__restrict__ p)
     }
 }
 
+// 8-byte aligned input (the open of bodies packed at 8-byte offsets): a
+// 16-byte chunk as two naturally aligned 8-byte loads.  ld16_8 reads the second half only when the
+// object reaches into it (an aligned 8-byte piece holding a valid byte cannot cross a page).
+__device__ __forceinline__ V4 ld16f_8(const uint8_t *__restrict__ p)
+{
+    const uint2 a = reinterpret_cast<const uint2 *>(p)[0], b = reinterpret_cast<const uint2 *>(p)[1];
+    return V4{a.x, a.y, b.x, b.y};
+}
+__device__ __forceinline__ V4 ld16_8(const uint8_t *__restrict__ p, u64 avail)
+{
+    if (avail == 0)
+        return zero4();
+    const uint2 a = reinterpret_cast<const uint2 *>(p)[0];
+    const uint2 b = avail > 8u ? reinterpret_cast<const uint2 *>(p)[1] : make_uint2(0u, 0u);
+    return V4{a.x, a.y, b.x, b.y};
+}
+
 template <bool AL>
 __device__ __forceinline__ void st16(uint8_t *__restrict__ p, u32 a, u32 b, u32 c, u32 d)
 {
@@ -1875,10 +1892,23 @@ __device__ __forceinline__ OpenSeg open_seg_geom(u32 size, u32 b0, u32 b1)
 
 // Open box blocks [b0, b1) of one MESSAGE body whose header passed open_header.
 // Returns CZ_STATUS_OK or (whole frame, bad tag) CZ_STATUS_CRYPTO.
-template <bool AL, class EM>
+template <bool AL, class EM, bool AL8 = false>
 __device__ __forceinline__ u32 open_segment(const uint8_t *__restrict__ in, u32 size, const u32 key[8], u32 n0, u32 n1, u32 b0,
                             u32 b1, u32 *__restrict__ rec, u32 &flags_out, EM &em)
 {
+    // AL: input 16-byte aligned; AL8: 8-byte aligned (two 8-byte loads per chunk); else any
+    auto ldf = [&](const uint8_t *p) -> V4 {
+        if constexpr (AL8)
+            return ld16f_8(p);
+        else
+            return ld16f<AL>(p);
+    };
+    auto ldp = [&](const uint8_t *p, u64 avail) -> V4 {
+        if constexpr (AL8)
+            return ld16_8(p, avail);
+        else
+            return ld16<AL>(p, avail);
+    };
     const OpenSeg g = open_seg_geom(size, b0, b1);
     const u32 mlen = size;
     const u32 nfull = mlen >> 6;
@@ -1889,8 +1919,8 @@ __device__ __forceinline__ u32 open_segment(const uint8_t *__restrict__ in, u32 
     u32 mpoly = 0;
     // prologue: plaintext dwords 8..15 of block cb (MACed here only for segment 0)
     if (b0 == 0) {
-        V4 a = ld16<AL>(in + 32, size > 32 ? size - 32u : 0);
-        V4 b = ld16<AL>(in + 48, size > 48 ? size - 48u : 0);
+        V4 a = ldp(in + 32, size > 32 ? size - 32u : 0);
+        V4 b = ldp(in + 48, size > 48 ? size - 48u : 0);
         const u32 nb = (mlen < 64u ? mlen : 64u) - 32u;
         if (nb >= 16u) {
             poly_block(P, a.x, a.y, a.z, a.w, 1u);
@@ -1912,7 +1942,7 @@ __device__ __forceinline__ u32 open_segment(const uint8_t *__restrict__ in, u32 
     } else {
         salsa20_block(X, key, n0, n1, g.cb, 0u);
         const uint8_t *src = in + 64u * g.cb + 32u;
-        V4 a = ld16f<AL>(src), b = ld16f<AL>(src + 16);
+        V4 a = ldf(src), b = ldf(src + 16);
         K[0] = a.x ^ X[8]; K[1] = a.y ^ X[9]; K[2] = a.z ^ X[10]; K[3] = a.w ^ X[11];
         K[4] = b.x ^ X[12]; K[5] = b.y ^ X[13]; K[6] = b.z ^ X[14]; K[7] = b.w ^ X[15];
     }
@@ -1923,13 +1953,13 @@ __device__ __forceinline__ u32 open_segment(const uint8_t *__restrict__ in, u32 
             V4 q0, q1, q2, q3;
             const bool full = blk < nfull;
             if (full) {
-                q0 = ld16f<AL>(src); q1 = ld16f<AL>(src + 16); q2 = ld16f<AL>(src + 32); q3 = ld16f<AL>(src + 48);
+                q0 = ldf(src); q1 = ldf(src + 16); q2 = ldf(src + 32); q3 = ldf(src + 48);
             } else {
                 const u32 o = 64u * blk;
-                q0 = ld16<AL>(src, size - o);
-                q1 = ld16<AL>(src + 16, o + 16u < size ? size - o - 16u : 0);
-                q2 = ld16<AL>(src + 32, o + 32u < size ? size - o - 32u : 0);
-                q3 = ld16<AL>(src + 48, o + 48u < size ? size - o - 48u : 0);
+                q0 = ldp(src, size - o);
+                q1 = ldp(src + 16, o + 16u < size ? size - o - 16u : 0);
+                q2 = ldp(src + 32, o + 32u < size ? size - o - 32u : 0);
+                q3 = ldp(src + 48, o + 48u < size ? size - o - 48u : 0);
             }
             u32 C[16] = {q0.x, q0.y, q0.z, q0.w, q1.x, q1.y, q1.z, q1.w,
                          q2.x, q2.y, q2.z, q2.w, q3.x, q3.y, q3.z, q3.w};
@@ -2260,6 +2290,7 @@ __device__ __forceinline__ bool wave_lines_ok(bool full_wave, u32 nchunks, bool 
 }
 
 constexpr int SEGMODE_REST = 4;   // k_seal_segments: only the waves k_seal_segments_lines leaves
+constexpr int SEGMODE_SHIFT16 = 8;  // 16-byte aligned outputs not all on 128-byte lines: EmitShiftLines
 
 // Segment kernels.  With line staging and whole-line loads enabled the launcher runs two
 // kernels over the same segment list: k_seal_segments_lines takes every full wave of aligned
@@ -2313,7 +2344,12 @@ __device__ __forceinline__ void seal_segments_body(const cz_frame_desc *__restri
             const u32 lane = threadIdx.x & 63u;
             uint8_t *wl = reinterpret_cast<uint8_t *>(smem) + (threadIdx.x >> 6) * SHIFT_LDS_BYTES;
             if (PART == SEGPART_LINES || pair) {
-                if (__builtin_amdgcn_ballot_w64(!al) == 0) {
+                // EmitSegLines stores 128-byte groups at each output's own base, which straddle two
+                // cache lines unless the base is line-aligned; EmitShiftLines stores whole cache
+                // lines at any base (SEGMODE_SHIFT16 sends it the 16-byte aligned waves too)
+                const bool line_al = (((uintptr_t)dst) & 127u) == 0;
+                if (__builtin_amdgcn_ballot_w64(!al) == 0 &&
+                    (!(mode & SEGMODE_SHIFT16) || __builtin_amdgcn_ballot_w64(!line_al) == 0)) {
                     EmitSegLines em{reinterpret_cast<uint4 *>(wl), dst, lane, total, 0u, 0u};
                     em.init(sg.first_block == 0);
                     seal_segment<true, EmitSegLines, true>(src, d.len, d.flags & 0xffu, d.counter, key,
@@ -2437,20 +2473,28 @@ __global__ __launch_bounds__(BLOCK) CZ_OPEN_SEG_OCC void k_open_segments(const c
     const u32 total = early == CZ_STATUS_OK ? (g.bend == g.nblk ? g.nout : 64u * g.ce) - 64u * g.cb : 0u;
     const bool al = aligned16(src, dst);
     const bool in_al = (((uintptr_t)src) & 15u) == 0;  // the line emitter takes outputs at any byte offset
+    // bodies at 8-byte offsets take the line emitters too, reading with 8-byte loads (lane-wise
+    // byte-exact stores ran them at ~1030 GiB/s on the Zipf batch)
+    const bool in_al8 = (((uintptr_t)src) & 7u) == 0;
     u32 fl = 0;
-    if (allow_lines && wave_lines_ok(wave_first + 64u <= nseg, nch, in_al) &&
+    if (allow_lines && wave_lines_ok(wave_first + 64u <= nseg, nch, in_al8) &&
         __builtin_amdgcn_ballot_w64(early != CZ_STATUS_OK) == 0) {
         const u32 lane = threadIdx.x & 63u;
         uint8_t *wl = reinterpret_cast<uint8_t *>(smem) + (threadIdx.x >> 6) * SHIFT_LDS_BYTES;
         u32 st;
-        if (__builtin_amdgcn_ballot_w64(!al) == 0) {
+        const bool line_al = (((uintptr_t)dst) & 127u) == 0;  // as in seal_segments_body
+        if (__builtin_amdgcn_ballot_w64(!al) == 0 &&
+            (!(mode & SEGMODE_SHIFT16) || __builtin_amdgcn_ballot_w64(!line_al) == 0)) {
             EmitSegLines em{reinterpret_cast<uint4 *>(wl), dst, lane, total, 0u, 0u};
             em.init(false);
             st = open_segment<true>(src, d.len, key, n0, n1, sg.first_block, b1, rec, fl, em);
         } else {  // plaintext at any byte offset
             EmitShiftLines em{wl, dst, lane, total, 0u, 0u};
             em.init(false);
-            st = open_segment<true>(src, d.len, key, n0, n1, sg.first_block, b1, rec, fl, em);
+            if (__builtin_amdgcn_ballot_w64(!in_al) == 0)
+                st = open_segment<true>(src, d.len, key, n0, n1, sg.first_block, b1, rec, fl, em);
+            else
+                st = open_segment<false, EmitShiftLines, true>(src, d.len, key, n0, n1, sg.first_block, b1, rec, fl, em);
         }
         if (!rec)
             status[sg.frame] = (uint16_t)(st | (st == CZ_STATUS_OK ? (fl << 8) : 0u));
@@ -2918,6 +2962,13 @@ static int g_pair = 1;
 static int g_un0 = 1;  // scalar first Salsa round when the high nonce word is wave-uniform
 static int g_seglines = 1;  // line-staged stores for waves of equal-length segments
 static int g_shift = 1;     // uniform seal: shifted line staging for bodies at any byte offset
+// segment kernels: waves of 16-byte aligned outputs that are not all on 128-byte lines go through
+// EmitShiftLines (whole cache lines) instead of EmitSegLines (128-byte groups at each output's
+// base, two partial cache lines per group): Zipf seal with 16-byte output slots 1250 -> 1629 GiB/s
+#ifndef CZ_SHIFT16_DEFAULT
+#define CZ_SHIFT16_DEFAULT 1
+#endif
+static int g_shift16 = CZ_SHIFT16_DEFAULT;
 
 // ---------------------------------------------------------------------------
 // Launchers (called from cz_host.cpp).  No allocation, no synchronisation:
@@ -3079,7 +3130,7 @@ hipError_t czk_seal_segments(const cz_frame_desc *desc, const cz_segment *segs, 
 #else
     if (nseg && g_seglines && g_pair) {
 #endif
-        const int mode = SEGMODE_LINES | SEGMODE_PAIR;
+        const int mode = SEGMODE_LINES | SEGMODE_PAIR | (g_shift16 ? SEGMODE_SHIFT16 : 0);
         hipLaunchKernelGGL(k_seal_segments_lines, grid, dim3(BLOCK), WAVES * SHIFT_LDS_BYTES, s, desc, segs, nseg,
                            (const uint8_t *)in, (uint8_t *)out, (const uint8_t *)subkeys, (u32 *)work, mode);
         hipLaunchKernelGGL(k_seal_segments, grid, dim3(BLOCK), 0, s, desc, segs, nseg, (const uint8_t *)in,
@@ -3102,7 +3153,8 @@ hipError_t czk_open_segments(const cz_frame_desc *desc, const cz_segment *segs, 
     if (nseg)
         hipLaunchKernelGGL(k_open_segments, dim3((nseg + BLOCK - 1) / BLOCK), dim3(BLOCK), WAVES * SHIFT_LDS_BYTES, s,
                            desc, segs, nseg, (const uint8_t *)in, (uint8_t *)out, (const uint8_t *)subkeys,
-                           (u32 *)work, status, nonces, (g_seglines ? SEGMODE_LINES : 0) | (g_pair ? SEGMODE_PAIR : 0));
+                           (u32 *)work, status, nonces,
+                           (g_seglines ? SEGMODE_LINES : 0) | (g_pair ? SEGMODE_PAIR : 0) | (g_shift16 ? SEGMODE_SHIFT16 : 0));
     if (ncomb)
         hipLaunchKernelGGL(k_open_combine, dim3((ncomb + BLOCK - 1) / BLOCK), dim3(BLOCK), 0, s, desc, comb, ncomb,
                            (const uint8_t *)in, (uint8_t *)out, (const u32 *)work, status);
@@ -3136,6 +3188,11 @@ int czk_tune(const char *key, int value)
     if (__builtin_strcmp(key, "seglines") == 0) {
         int old = g_seglines;
         g_seglines = value != 0;
+        return old;
+    }
+    if (__builtin_strcmp(key, "shift16") == 0) {
+        int old = g_shift16;
+        g_shift16 = value != 0;
         return old;
     }
     if (__builtin_strcmp(key, "shift") == 0) {

@@ -124,12 +124,13 @@ def _bodies(lens, seed):
     return bodies, meta
 
 
-def _bodies_desc(bodies, meta, shift=0):
+def _bodies_desc(bodies, meta, shift=0, pack=16):
+    """pack: body slot granularity (8 with shift 0 = SURVEY.md 8(d) row 4's 8-byte offset table)"""
     desc = np.zeros(len(bodies), dtype=DESC_DTYPE)
     io, oo = shift, 3 if shift else 0
     for i, b in enumerate(bodies):
         desc[i] = (io, oo, len(b), meta[i][3], meta[i][2] - 1, 0x100, -1)
-        io += (len(b) + 15) // 16 * 16
+        io += (len(b) + pack - 1) // pack * pack
         oo += (max(len(b) - 33, 0) + 15) // 16 * 16
     hin = np.zeros(io + 64, dtype=np.uint8)
     for i, b in enumerate(bodies):
@@ -233,6 +234,53 @@ def test_zipf_seal_open_line_and_direct_stores(torch_dev, subkeys, L, seglines, 
     finally:
         lib.cz_tune(b"seglines", old)
         lib.cz_tune(b"pair", old_pair)
+
+
+@pytest.mark.parametrize("shift16", [1, 0])
+def test_zipf_open_8byte_bodies_and_16byte_outputs(torch_dev, subkeys, L, shift16):
+    """Line-emitter paths by alignment (cz_tune "shift16": 16-byte aligned outputs off the 128-byte
+    lines through EmitShiftLines): a Zipf batch sealed into 16-byte slots vs the oracle, then its
+    bodies repacked at 8-byte offsets (the open's 8-byte-load lines path) and opened with tampered
+    and replayed frames mixed in; rejected frames leave zeros."""
+    lib = L.lib()
+    old = lib.cz_tune(b"shift16", shift16)
+    try:
+        rng = np.random.default_rng(23 + shift16)
+        j = np.clip(rng.zipf(1.2, size=3000), 1, 1024)
+        lens = [int(x) for x in (64 * j - rng.integers(0, 64, size=len(j)))]
+        desc, hin, ob = _pack(lens, seed=29)
+        assert (desc["out_off"] % 16 == 0).all() and (desc["out_off"] % 128 != 0).any()
+        out, _ = _seal_seg(torch_dev, subkeys, desc, hin, ob, 64)
+        assert np.array_equal(out, _oracle_seal(desc, hin, ob))
+        bodies, meta = [], []
+        for i, n in enumerate(lens):
+            o = int(desc[i]["out_off"])
+            bodies.append(bytearray(out[o:o + n + 33].tobytes()))
+            o_in = int(desc[i]["in_off"])
+            meta.append((hin[o_in:o_in + n].tobytes(), int(desc[i]["flags"]), int(desc[i]["counter"]), 0))
+        want = [L.CZ_STATUS_OK] * len(bodies)
+        for i in rng.choice(len(bodies), size=40, replace=False):
+            b = bodies[i]
+            b[int(rng.integers(16, len(b)))] ^= 0x04
+            want[i] = L.CZ_STATUS_CRYPTO
+        odesc, ohin, oob = _bodies_desc(bodies, meta, pack=8)
+        assert (odesc["in_off"] % 16 == 8).any()
+        for i in rng.choice(len(bodies), size=10, replace=False):
+            if want[i] == L.CZ_STATUS_OK:
+                odesc[i]["counter"] = meta[i][2] + 1
+                want[i] = L.CZ_STATUS_SEQUENCE
+        st, pout, nn, plan = _open_seg(torch_dev, subkeys, odesc, ohin, oob, 64)
+        assert list(st & 0xff) == want
+        for i, (p, fl, ctr, k) in enumerate(meta):
+            o = int(odesc[i]["out_off"])
+            if want[i] == L.CZ_STATUS_OK:
+                assert st[i] >> 8 == fl
+                assert pout[o:o + len(p)].tobytes() == p, f"frame {i} len {len(p)}"
+            elif want[i] == L.CZ_STATUS_CRYPTO:
+                assert not pout[o:o + len(p)].any()
+            assert nn[i] == ctr
+    finally:
+        lib.cz_tune(b"shift16", old)
 
 
 def test_full_size_zipf_roundtrip(torch_dev, subkeys, L):

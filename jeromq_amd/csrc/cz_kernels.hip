@@ -118,6 +118,7 @@ typedef __attribute__((address_space(1))) u64_ua g_u64_ua;
 typedef __attribute__((address_space(1))) u32_ua g_u32_ua;
 typedef __attribute__((address_space(1))) u16_ua g_u16_ua;
 typedef v4u_t v4u_ua __attribute__((aligned(1)));
+typedef uint4 u4_a4 __attribute__((aligned(4)));  // a 16-byte load from a dword-aligned address
 typedef __attribute__((address_space(1))) v4u_ua g_v4u_ua;
 
 // 16-byte line store through a buffer resource: `base` wave-uniform (SGPRs), `voff` this lane's
@@ -893,11 +894,40 @@ __device__ __forceinline__ void seal_frame(const uint8_t *__restrict__ in, u32 n
 // On a bad tag the emitted plaintext is overwritten with zeros (em.poison()).
 // Frames rejected before decryption emit nothing.
 // --------------------------------------------------------------------------
-template <int MODE, bool AL, class EM, bool PAIR = false, bool UN0 = false, bool LAZY = true>
+// INA: the input's alignment class.  16: 16-byte aligned (AL as given); 8 and 1 (AL true): bodies at
+// any byte offset (the dense wire layout, V2Decoder.java:67-105 leaves bodies back to back), read
+// with 16-byte loads from the dword-aligned address at or below and, for 1, one
+// v_alignbyte_b32 per dword by (in & 3) with the dword after the 16 bytes (loaded only when
+// in & 3 != 0); a whole line is 8 such loads plus that dword.  A chunk whose 16 bytes are all in
+// the body never reads past the dword holding its last byte (a dword cannot cross a page) nor
+// below the body's first dword (the buffer base is dword-aligned).
+template <int MODE, bool AL, class EM, bool PAIR = false, bool UN0 = false, bool LAZY = true, int INA = 16>
 __device__ __forceinline__ u32 open_frame(const uint8_t *__restrict__ in, u32 size, const u32 key[8],
                                           bool check_floor, long long floor, u32 *flags_out, u64 *nonce_out,
                                           u64 nacl_counter, EM &em)
 {
+    static_assert(INA == 16 || (AL && (INA == 8 || INA == 1)), "INA 8/1 take the AL code paths");
+    const u32 ina = INA == 1 ? (u32)(uintptr_t)in & 3u : 0u;
+    const uint8_t *in4 = in - ina;
+    // the 16 box bytes at `off`, every one inside the body
+    auto LF = [&](u32 off) -> V4 {
+        if constexpr (INA == 16) {
+            return ld16f<AL>(in + off);
+        } else {
+            const uint4 r = *reinterpret_cast<const u4_a4 *>(in4 + off);
+            if constexpr (INA == 8)
+                return V4{r.x, r.y, r.z, r.w};
+            const u32 r4 = ina ? *reinterpret_cast<const u32 *>(in4 + off + 16) : 0u;
+            return V4{funnel(r.y, r.x, ina), funnel(r.z, r.y, ina), funnel(r.w, r.z, ina), funnel(r4, r.w, ina)};
+        }
+    };
+    // the box bytes at `off`, avail of them inside the body
+    auto LP = [&](u32 off, u64 avail) -> V4 {
+        if constexpr (INA == 16)
+            return ld16<AL>(in + off, avail);
+        else
+            return avail >= 16u ? LF(off) : ld16<false>(in + off, avail);
+    };
     // A cooperative emitter needs every lane of the wave in the same chunk
     // sequence: a frame rejected before decryption then runs through the
     // (uniform-size) loop as a dead lane that emits zeros.
@@ -907,7 +937,7 @@ __device__ __forceinline__ u32 open_frame(const uint8_t *__restrict__ in, u32 si
     if constexpr (MODE == MODE_ZMQ) {
         // Msgs.startsWith(msg, "MESSAGE", true) (zmq/io/Msgs.java:20-39): size >= 8,
         // byte 0 == 7, bytes 1..6 == "MESSAG" (its loop never reaches byte 7).
-        V4 h = ld16<AL>(in, size);
+        V4 h = LP(0, size);
         if (size < 8u || h.x != HDR0 || (h.y & 0x00ffffffu) != (HDR1 & 0x00ffffffu))
             early = CZ_STATUS_COMMAND;
         else if (size < 33u)
@@ -968,12 +998,12 @@ __device__ __forceinline__ u32 open_frame(const uint8_t *__restrict__ in, u32 si
     [[maybe_unused]] u32 L1[16];
     if constexpr (EARLY0) {
         if (early0) {
-            e_tin = ld16f<AL>(in + 16);
-            e_a = ld16f<AL>(in + 32);
-            e_b = ld16f<AL>(in + 48);
+            e_tin = LF(16);
+            e_a = LF(32);
+            e_b = LF(48);
 #pragma unroll
             for (int c = 0; c < 4; c++) {
-                V4 v = ld16f<AL>(in + 64 + 16 * c);
+                V4 v = LF(64 + 16 * c);
                 L1[4 * c] = v.x; L1[4 * c + 1] = v.y; L1[4 * c + 2] = v.z; L1[4 * c + 3] = v.w;
             }
         }
@@ -982,7 +1012,7 @@ __device__ __forceinline__ u32 open_frame(const uint8_t *__restrict__ in, u32 si
     ksblock(x, 0u, 0u);
     Poly P;
     poly_init(P, x[0], x[1], x[2], x[3], x[4], x[5], x[6], x[7]);
-    V4 tin = early0 ? e_tin : ld16<AL>(in + 16, size - 16u);
+    V4 tin = early0 ? e_tin : LP(16, size - 16u);
 
     // ZMQ: payload chunk m (bytes [64m, 64m+64)) = box [64m+33, 64m+97): dword t is
     // alignbyte(D[16m+t+9], D[16m+t+8], 1), D = plaintext box dwords.  It is emitted
@@ -991,8 +1021,8 @@ __device__ __forceinline__ u32 open_frame(const uint8_t *__restrict__ in, u32 si
 
     // block 0
     {
-        V4 a = early0 ? e_a : ld16<AL>(in + 32, size > 32 ? size - 32u : 0);
-        V4 b = early0 ? e_b : ld16<AL>(in + 48, size > 48 ? size - 48u : 0);
+        V4 a = early0 ? e_a : LP(32, size > 32 ? size - 32u : 0);
+        V4 b = early0 ? e_b : LP(48, size > 48 ? size - 48u : 0);
         C[8] = a.x; C[9] = a.y; C[10] = a.z; C[11] = a.w;
         C[12] = b.x; C[13] = b.y; C[14] = b.z; C[15] = b.w;
         if (nfull >= 1) {
@@ -1080,12 +1110,26 @@ __device__ __forceinline__ u32 open_frame(const uint8_t *__restrict__ in, u32 si
             open_block(1, true);
             blk = 2;
             for (u32 k = 1; 2u * k + 1u < nfull; k++) {
-                const uint8_t *src = in + 128u * k;
                 u32 M[32];
+                if constexpr (INA == 1) {
+                    // 8 loads from the dword-aligned line below and the dword after it, funnelled
+                    const uint8_t *src4 = in4 + 128u * k;
+                    u32 R[33];
 #pragma unroll
-                for (int c = 0; c < 8; c++) {
-                    V4 v = ld16f<AL>(src + 16 * c);
-                    M[4 * c] = v.x; M[4 * c + 1] = v.y; M[4 * c + 2] = v.z; M[4 * c + 3] = v.w;
+                    for (int c = 0; c < 8; c++) {
+                        const uint4 v = *reinterpret_cast<const u4_a4 *>(src4 + 16 * c);
+                        R[4 * c] = v.x; R[4 * c + 1] = v.y; R[4 * c + 2] = v.z; R[4 * c + 3] = v.w;
+                    }
+                    R[32] = ina ? *reinterpret_cast<const u32 *>(src4 + 128) : 0u;  // (2k+2 <= nfull)
+#pragma unroll
+                    for (int q = 0; q < 32; q++)
+                        M[q] = funnel(R[q + 1], R[q], ina);
+                } else {
+#pragma unroll
+                    for (int c = 0; c < 8; c++) {
+                        V4 v = LF(128u * k + 16u * c);
+                        M[4 * c] = v.x; M[4 * c + 1] = v.y; M[4 * c + 2] = v.z; M[4 * c + 3] = v.w;
+                    }
                 }
 #pragma unroll
                 for (int q = 0; q < 16; q++)
@@ -1103,18 +1147,19 @@ __device__ __forceinline__ u32 open_frame(const uint8_t *__restrict__ in, u32 si
         const uint8_t *src = in + 64u * blk;
         V4 q0, q1, q2, q3;
         const bool full = blk < nfull;
+        const u32 o = 64u * blk;
         if (full) {
-            q0 = ld16f<AL>(src);
-            q1 = ld16f<AL>(src + 16);
-            q2 = ld16f<AL>(src + 32);
-            q3 = ld16f<AL>(src + 48);
+            q0 = LF(o);
+            q1 = LF(o + 16u);
+            q2 = LF(o + 32u);
+            q3 = LF(o + 48u);
         } else {
-            const u32 o = 64u * blk;
-            q0 = ld16<AL>(src, size - o);
-            q1 = ld16<AL>(src + 16, o + 16u < size ? size - o - 16u : 0);
-            q2 = ld16<AL>(src + 32, o + 32u < size ? size - o - 32u : 0);
-            q3 = ld16<AL>(src + 48, o + 48u < size ? size - o - 48u : 0);
+            q0 = LP(o, size - o);
+            q1 = LP(o + 16u, o + 16u < size ? size - o - 16u : 0);
+            q2 = LP(o + 32u, o + 32u < size ? size - o - 32u : 0);
+            q3 = LP(o + 48u, o + 48u < size ? size - o - 48u : 0);
         }
+        (void)src;
         C[0] = q0.x; C[1] = q0.y; C[2] = q0.z; C[3] = q0.w;
         C[4] = q1.x; C[5] = q1.y; C[6] = q1.z; C[7] = q1.w;
         C[8] = q2.x; C[9] = q2.y; C[10] = q2.z; C[11] = q2.w;
@@ -2192,13 +2237,16 @@ __global__ __launch_bounds__(BLOCK) void k_open_desc(const cz_frame_desc *__rest
 
 // Uniform open of one connection's bodies in order: frame i must beat frame
 // i-1's nonce, frame 0 must beat floor0 (when check != 0).
-template <int ST, bool PAIR>
+// INA (open_frame): 16 for 16-byte aligned bodies; 8 / 1 for bodies at 8-byte / any byte offsets
+// (the dense wire layout), line-staged (ST_LINES) plaintext only
+template <int ST, bool PAIR, int INA = 16>
 __global__ __launch_bounds__(BLOCK) CZ_OCC void k_open_uniform(const uint8_t *__restrict__ in, uint64_t in_stride,
                                                          uint8_t *__restrict__ out, uint64_t out_stride,
                                                          uint32_t count, uint32_t size,
                                                          const uint8_t *__restrict__ subkey, uint64_t floor0,
                                                          int check, uint16_t *__restrict__ status, int allow_un0)
 {
+    static_assert(INA == 16 || ST == ST_LINES, "unaligned bodies: line-staged plaintext only");
     extern __shared__ uint4 smem[];
     const uint32_t i = blockIdx.x * BLOCK + threadIdx.x;
     const uint32_t wave_first = i & ~63u;
@@ -2217,21 +2265,25 @@ __global__ __launch_bounds__(BLOCK) CZ_OCC void k_open_uniform(const uint8_t *__
         // (16-byte aligned slots here: the previous body's nonce is one 8-byte load, not 8 byte loads)
         long long floor = (long long)floor0;
         if (i > 0) {
-            const uint2 pn = *reinterpret_cast<const uint2 *>(src - in_stride + 8);
-            floor = (long long)(((u64)bswap32(pn.x) << 32) | (u64)bswap32(pn.y));
+            if constexpr (INA >= 8) {
+                const uint2 pn = *reinterpret_cast<const uint2 *>(src - in_stride + 8);
+                floor = (long long)(((u64)bswap32(pn.x) << 32) | (u64)bswap32(pn.y));
+            } else {
+                floor = (long long)read_be64(src - in_stride + 8);
+            }
         }
         const u32 lane = threadIdx.x & 63u;
-        const bool un0 = allow_un0 && wave_uniform(*reinterpret_cast<const u32 *>(src + 8));
+        const bool un0 = allow_un0 && wave_uniform(INA >= 8 ? *reinterpret_cast<const u32 *>(src + 8) : ld32<false>(src + 8));
         if constexpr (ST == ST_LINES) {
             EmitLines em{smem + (threadIdx.x >> 6) * (LINE_LDS_BYTES / 16), out + (uint64_t)wave_first * out_stride,
                          dst, out_stride, lane, nout, 0u, false};
             if (un0)
-                st = open_frame<MODE_ZMQ, true, EmitLines, PAIR, true>(src, size, key, check != 0, floor, &fl, &nonce,
-                                                                      0, em);
+                st = open_frame<MODE_ZMQ, true, EmitLines, PAIR, true, true, INA>(src, size, key, check != 0, floor, &fl,
+                                                                                 &nonce, 0, em);
             else
-                st = open_frame<MODE_ZMQ, true, EmitLines, PAIR, false>(src, size, key, check != 0, floor, &fl, &nonce,
-                                                                       0, em);
-        } else {
+                st = open_frame<MODE_ZMQ, true, EmitLines, PAIR, false, true, INA>(src, size, key, check != 0, floor, &fl,
+                                                                                  &nonce, 0, em);
+        } else if constexpr (INA == 16) {
             const u32 ost = (u32)out_stride;
             EmitRegion em{smem + (threadIdx.x >> 6) * ((64u * ost) >> 4), out + (uint64_t)wave_first * out_stride,
                           ost, lane, nout};
@@ -2962,6 +3014,7 @@ static int g_pair = 1;
 static int g_un0 = 1;  // scalar first Salsa round when the high nonce word is wave-uniform
 static int g_seglines = 1;  // line-staged stores for waves of equal-length segments
 static int g_shift = 1;     // uniform seal: shifted line staging for bodies at any byte offset
+static int g_open_ina = 1;  // uniform open: line path for bodies off 16-byte alignment (dword-aligned loads)
 // segment kernels: waves of 16-byte aligned outputs that are not all on 128-byte lines go through
 // EmitShiftLines (whole cache lines) instead of EmitSegLines (128-byte groups at each output's
 // base, two partial cache lines per group): Zipf seal with 16-byte output slots 1250 -> 1629 GiB/s
@@ -3067,8 +3120,24 @@ hipError_t czk_open_uniform(const void *in, uint64_t in_stride, void *out, uint6
 #define CZ_OPEN_LAUNCH(ST, PR, LDS)                                                                        \
     hipLaunchKernelGGL((k_open_uniform<ST, PR>), grid, dim3(BLOCK), (LDS), s, (const uint8_t *)in, in_stride,   \
                        (uint8_t *)out, out_stride, count, size, (const uint8_t *)subkey, floor0, check, status, g_un0)
+#define CZ_OPEN_LAUNCH_INA(INA)                                                                              \
+    hipLaunchKernelGGL((k_open_uniform<ST_LINES, true, INA>), grid, dim3(BLOCK), WAVES * LINE_LDS_BYTES, s,        \
+                       (const uint8_t *)in, in_stride, (uint8_t *)out, out_stride, count, size,                    \
+                       (const uint8_t *)subkey, floor0, check, status, g_un0)
     const int st = size >= 33u ? pick_staging(out_stride, nout, al) : (int)ST_DIRECT;
     const unsigned lds = st == ST_LINES ? WAVES * LINE_LDS_BYTES : (st == ST_REGION ? (unsigned)(WAVES * 64 * out_stride) : 0u);
+    // bodies off 16-byte alignment (the dense wire layout) into line-aligned plaintext slots: the
+    // line path with dword-aligned loads (INA 8 / 1) instead of lane-wise byte-exact stores
+    const bool out_al = ((((uintptr_t)out | out_stride) & 15u) == 0);
+    const int st_out = size >= 33u ? pick_staging(out_stride, nout, out_al) : (int)ST_DIRECT;
+    if (g_pair && !al && st_out == ST_LINES && g_open_ina) {
+        const uint64_t ia = (uintptr_t)in | in_stride;
+        if ((ia & 7u) == 0)
+            CZ_OPEN_LAUNCH_INA(8);
+        else
+            CZ_OPEN_LAUNCH_INA(1);
+        return hipGetLastError();
+    }
     if (g_pair && st != ST_REGION) {
         if (st == ST_LINES) CZ_OPEN_LAUNCH(ST_LINES, true, lds);
         else CZ_OPEN_LAUNCH(ST_DIRECT, true, 0);
@@ -3078,6 +3147,7 @@ hipError_t czk_open_uniform(const void *in, uint64_t in_stride, void *out, uint6
         else CZ_OPEN_LAUNCH(ST_DIRECT, false, 0);
     }
 #undef CZ_OPEN_LAUNCH
+#undef CZ_OPEN_LAUNCH_INA
     return hipGetLastError();
 }
 
@@ -3188,6 +3258,11 @@ int czk_tune(const char *key, int value)
     if (__builtin_strcmp(key, "seglines") == 0) {
         int old = g_seglines;
         g_seglines = value != 0;
+        return old;
+    }
+    if (__builtin_strcmp(key, "open_ina") == 0) {
+        int old = g_open_ina;
+        g_open_ina = value != 0;
         return old;
     }
     if (__builtin_strcmp(key, "shift16") == 0) {

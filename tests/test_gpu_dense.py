@@ -157,3 +157,49 @@ def test_open_segments_dense_plaintext(torch_dev, subkeys, out_round):
         assert out[s:s + len(p)].tobytes() == p, f"frame {i} (len {len(p)}) plaintext differs"
         spans.append((s, s + len(p)))
     _gaps_untouched(out, spans, 0, ob)
+
+
+@pytest.mark.parametrize("n,stride", [(4096, 4129), (4096, 4130), (4096, 4131), (4096, 4136), (4096, 4144),
+                                      (300, 333), (1000, 1041)])
+@pytest.mark.parametrize("base", [0, 1, 8, 13])
+def test_open_uniform_any_offset(torch_dev, subkeys, n, stride, base):
+    """cz_open_uniform of bodies back to back at any byte phase (the receive side of the dense wire
+    layout: V2Decoder.java:67-105 leaves bodies back to back; CurveClientMechanism.decode,
+    :165-224) into line-aligned plaintext slots: the line path with dword-aligned loads.  Tampered
+    frames report CZ_STATUS_CRYPTO and leave zeros; every other payload and flags byte comes back."""
+    torch, dev = torch_dev
+    from jeromq_amd import _lib, batch
+    count = 64 * 5 + 17
+    in_stride = (n + 15) // 16 * 16
+    hin = np.frombuffer(splitmix_bytes(count * in_stride, 2000 + n + stride), dtype=np.uint8).copy()
+    d_in = torch.from_numpy(hin).to(dev)
+    size = base + count * stride + 64
+    d_buf = torch.full((size,), SENTINEL, dtype=torch.uint8, device=dev)
+    d_bodies = d_buf[base:]
+    flags = torch.tensor([(i % 3 == 0) | (2 if i % 5 == 0 else 0) for i in range(count)], dtype=torch.uint8, device=dev)
+    c0 = 0xFFFFFFF0 - 100  # the high nonce word changes inside a wave
+    batch.seal_uniform(d_in, in_stride, d_bodies, stride, count, n, subkeys[0], c0, flags8=flags)
+    torch.cuda.synchronize()
+    bodies = d_buf.cpu().numpy()
+    rng = np.random.default_rng(n + stride + base)
+    bad = sorted(int(x) for x in rng.choice(count, size=9, replace=False))
+    for j, i in enumerate(bad):  # tag, first / middle / last ciphertext byte
+        where = [16 + j % 16, 33, (n + 33) // 2, n + 32][j % 4]
+        bodies[base + i * stride + where] ^= 1 << (j % 8)
+    d_buf.copy_(torch.from_numpy(bodies))
+    plain_stride = (n + 127) // 128 * 128
+    d_plain = torch.full((count * plain_stride,), SENTINEL, dtype=torch.uint8, device=dev)
+    status = torch.full((count,), -1, dtype=torch.int16, device=dev)
+    batch.open_uniform(d_bodies, stride, d_plain, plain_stride, count, n + 33, subkeys[0], c0 - 1, status)
+    torch.cuda.synchronize()
+    st = status.cpu().numpy().view(np.uint16)
+    plain = d_plain.cpu().numpy()
+    fl = flags.cpu().numpy()
+    for i in range(count):
+        p = plain[i * plain_stride:i * plain_stride + n]
+        if i in bad:
+            assert st[i] & 0xff == _lib.CZ_STATUS_CRYPTO, f"frame {i}"
+            assert not p.any(), f"frame {i} leaked plaintext"
+        else:
+            assert st[i] & 0xff == _lib.CZ_STATUS_OK and st[i] >> 8 == fl[i], f"frame {i} status {st[i]:#x}"
+            assert p.tobytes() == hin[i * in_stride:i * in_stride + n].tobytes(), f"frame {i} (stride {stride}, base {base})"

@@ -82,6 +82,11 @@ constexpr int BLOCK = 256;              // threads per workgroup (4 waves)
 #define CZ_OPEN_SEG_WAVES_PER_EU 3
 #endif
 #define CZ_OPEN_SEG_OCC __attribute__((amdgpu_waves_per_eu(CZ_OPEN_SEG_WAVES_PER_EU, CZ_OPEN_SEG_WAVES_PER_EU)))
+#ifndef CZ_UNIFORM_WAVES_PER_EU
+#define CZ_OPEN_UNI_OCC __attribute__((amdgpu_waves_per_eu(3)))
+#else
+#define CZ_OPEN_UNI_OCC
+#endif
 #ifdef CZ_SEG_WAVES_PER_EU
 #define CZ_SEG_OCC __attribute__((amdgpu_waves_per_eu(CZ_SEG_WAVES_PER_EU, CZ_SEG_WAVES_PER_EU)))
 #else
@@ -2239,17 +2244,24 @@ __global__ __launch_bounds__(BLOCK) void k_open_desc(const cz_frame_desc *__rest
 // i-1's nonce, frame 0 must beat floor0 (when check != 0).
 // INA (open_frame): 16 for 16-byte aligned bodies; 8 / 1 for bodies at 8-byte / any byte offsets
 // (the dense wire layout), line-staged (ST_LINES) plaintext only
+// (at least 3 waves per SIMD: the byte-shifted plaintext staging needs 170-179 VGPRs uncapped)
 template <int ST, bool PAIR, int INA = 16>
-__global__ __launch_bounds__(BLOCK) CZ_OCC void k_open_uniform(const uint8_t *__restrict__ in, uint64_t in_stride,
+__global__ __launch_bounds__(BLOCK) CZ_OCC CZ_OPEN_UNI_OCC void k_open_uniform(const uint8_t *__restrict__ in, uint64_t in_stride,
                                                          uint8_t *__restrict__ out, uint64_t out_stride,
                                                          uint32_t count, uint32_t size,
                                                          const uint8_t *__restrict__ subkey, uint64_t floor0,
                                                          int check, uint16_t *__restrict__ status, int allow_un0)
 {
-    static_assert(INA == 16 || ST == ST_LINES, "unaligned bodies: line-staged plaintext only");
+    static_assert(INA == 16 || ST == ST_LINES || ST == ST_SHIFT, "unaligned bodies: line-staged plaintext only");
     extern __shared__ uint4 smem[];
-    const uint32_t i = blockIdx.x * BLOCK + threadIdx.x;
-    const uint32_t wave_first = i & ~63u;
+    uint32_t i = blockIdx.x * BLOCK + threadIdx.x;
+    if constexpr (ST == ST_SHIFT) {
+        // plaintext at any byte offset: a full workgroup's frames sorted by line class, as the seal
+        if (blockIdx.x * BLOCK + BLOCK <= count)
+            i = blockIdx.x * BLOCK + class_permute(((uintptr_t)(out + (uint64_t)i * out_stride) & 64u) != 0,
+                                                   reinterpret_cast<u32 *>(smem));
+    }
+    const uint32_t wave_first = (blockIdx.x * BLOCK + threadIdx.x) & ~63u;
     if (wave_first >= count)
         return;
     u32 key[8];
@@ -2283,6 +2295,17 @@ __global__ __launch_bounds__(BLOCK) CZ_OCC void k_open_uniform(const uint8_t *__
             else
                 st = open_frame<MODE_ZMQ, true, EmitLines, PAIR, false, true, INA>(src, size, key, check != 0, floor, &fl,
                                                                                   &nonce, 0, em);
+        } else if constexpr (ST == ST_SHIFT) {
+            EmitShiftLinesUni em{reinterpret_cast<uint8_t *>(smem) + (threadIdx.x >> 6) * SHIFT_LDS_BYTES, dst, lane,
+                                 nout, 0u, 0u};
+            em.init(false);
+            em.init_uniform(i - blockIdx.x * BLOCK, (u32)out_stride, out + (uint64_t)blockIdx.x * BLOCK * out_stride);
+            if (un0)
+                st = open_frame<MODE_ZMQ, true, EmitShiftLinesUni, PAIR, true, true, INA>(src, size, key, check != 0,
+                                                                                         floor, &fl, &nonce, 0, em);
+            else
+                st = open_frame<MODE_ZMQ, true, EmitShiftLinesUni, PAIR, false, true, INA>(src, size, key, check != 0,
+                                                                                          floor, &fl, &nonce, 0, em);
         } else if constexpr (INA == 16) {
             const u32 ost = (u32)out_stride;
             EmitRegion em{smem + (threadIdx.x >> 6) * ((64u * ost) >> 4), out + (uint64_t)wave_first * out_stride,
@@ -3120,22 +3143,35 @@ hipError_t czk_open_uniform(const void *in, uint64_t in_stride, void *out, uint6
 #define CZ_OPEN_LAUNCH(ST, PR, LDS)                                                                        \
     hipLaunchKernelGGL((k_open_uniform<ST, PR>), grid, dim3(BLOCK), (LDS), s, (const uint8_t *)in, in_stride,   \
                        (uint8_t *)out, out_stride, count, size, (const uint8_t *)subkey, floor0, check, status, g_un0)
-#define CZ_OPEN_LAUNCH_INA(INA)                                                                              \
-    hipLaunchKernelGGL((k_open_uniform<ST_LINES, true, INA>), grid, dim3(BLOCK), WAVES * LINE_LDS_BYTES, s,        \
-                       (const uint8_t *)in, in_stride, (uint8_t *)out, out_stride, count, size,                    \
-                       (const uint8_t *)subkey, floor0, check, status, g_un0)
+#define CZ_OPEN_LAUNCH_INA(ST, INA, LDS)                                                                     \
+    hipLaunchKernelGGL((k_open_uniform<ST, true, INA>), grid, dim3(BLOCK), (LDS), s, (const uint8_t *)in,          \
+                       in_stride, (uint8_t *)out, out_stride, count, size, (const uint8_t *)subkey, floor0, check, \
+                       status, g_un0)
     const int st = size >= 33u ? pick_staging(out_stride, nout, al) : (int)ST_DIRECT;
     const unsigned lds = st == ST_LINES ? WAVES * LINE_LDS_BYTES : (st == ST_REGION ? (unsigned)(WAVES * 64 * out_stride) : 0u);
     // bodies off 16-byte alignment (the dense wire layout) into line-aligned plaintext slots: the
     // line path with dword-aligned loads (INA 8 / 1) instead of lane-wise byte-exact stores
     const bool out_al = ((((uintptr_t)out | out_stride) & 15u) == 0);
-    const int st_out = size >= 33u ? pick_staging(out_stride, nout, out_al) : (int)ST_DIRECT;
-    if (g_pair && !al && st_out == ST_LINES && g_open_ina) {
-        const uint64_t ia = (uintptr_t)in | in_stride;
-        if ((ia & 7u) == 0)
-            CZ_OPEN_LAUNCH_INA(8);
-        else
-            CZ_OPEN_LAUNCH_INA(1);
+    int st_out = size >= 33u ? pick_staging(out_stride, nout, out_al) : (int)ST_DIRECT;
+    // plaintext at any byte offset (slots that are not 128-byte multiples): byte-shifted line
+    // staging, as the seal's bodies (EmitShiftLinesUni; its buffer-store offsets stay below 2^31)
+    if (st_out == ST_DIRECT && size >= 33u && nout >= 256u && out_stride < (1ull << 22) && g_shift)
+        st_out = ST_SHIFT;
+    const uint64_t ia = (uintptr_t)in | in_stride;
+    const int ina = (ia & 15u) == 0 ? 16 : (ia & 7u) == 0 ? 8 : 1;
+    if (g_pair && (st_out == ST_SHIFT || (st_out == ST_LINES && ina != 16)) && (ina == 16 || g_open_ina)) {
+        if (st_out == ST_LINES) {
+            if (ina == 8)
+                CZ_OPEN_LAUNCH_INA(ST_LINES, 8, WAVES * LINE_LDS_BYTES);
+            else
+                CZ_OPEN_LAUNCH_INA(ST_LINES, 1, WAVES * LINE_LDS_BYTES);
+        } else if (ina == 16) {
+            CZ_OPEN_LAUNCH_INA(ST_SHIFT, 16, WAVES * SHIFT_LDS_BYTES);
+        } else if (ina == 8) {
+            CZ_OPEN_LAUNCH_INA(ST_SHIFT, 8, WAVES * SHIFT_LDS_BYTES);
+        } else {
+            CZ_OPEN_LAUNCH_INA(ST_SHIFT, 1, WAVES * SHIFT_LDS_BYTES);
+        }
         return hipGetLastError();
     }
     if (g_pair && st != ST_REGION) {

@@ -162,11 +162,14 @@ def test_open_segments_dense_plaintext(torch_dev, subkeys, out_round):
 @pytest.mark.parametrize("n,stride", [(4096, 4129), (4096, 4130), (4096, 4131), (4096, 4136), (4096, 4144),
                                       (300, 333), (1000, 1041)])
 @pytest.mark.parametrize("base", [0, 1, 8, 13])
-def test_open_uniform_any_offset(torch_dev, subkeys, n, stride, base):
+@pytest.mark.parametrize("layout", ["line", "shift"])
+def test_open_uniform_any_offset(torch_dev, subkeys, n, stride, base, layout):
     """cz_open_uniform of bodies back to back at any byte phase (the receive side of the dense wire
     layout: V2Decoder.java:67-105 leaves bodies back to back; CurveClientMechanism.decode,
     :165-224) into line-aligned plaintext slots: the line path with dword-aligned loads.  Tampered
-    frames report CZ_STATUS_CRYPTO and leave zeros; every other payload and flags byte comes back."""
+    frames report CZ_STATUS_CRYPTO and leave zeros; every other payload and flags byte comes back.
+    layout="shift": plaintext slots that are not 128-byte multiples, 5 bytes off the buffer's line
+    (byte-shifted line staging); the bytes between slots stay as the caller wrote them."""
     torch, dev = torch_dev
     from jeromq_amd import _lib, batch
     count = 64 * 5 + 17
@@ -187,13 +190,21 @@ def test_open_uniform_any_offset(torch_dev, subkeys, n, stride, base):
         where = [16 + j % 16, 33, (n + 33) // 2, n + 32][j % 4]
         bodies[base + i * stride + where] ^= 1 << (j % 8)
     d_buf.copy_(torch.from_numpy(bodies))
-    plain_stride = (n + 127) // 128 * 128
-    d_plain = torch.full((count * plain_stride,), SENTINEL, dtype=torch.uint8, device=dev)
+    if layout == "line":
+        plain_stride, pbase = (n + 127) // 128 * 128, 0
+    else:
+        plain_stride, pbase = (n + 16 if n % 128 == 0 else n), 5
+    d_pbuf = torch.full((pbase + count * plain_stride + 64,), SENTINEL, dtype=torch.uint8, device=dev)
+    d_plain = d_pbuf[pbase:]
     status = torch.full((count,), -1, dtype=torch.int16, device=dev)
     batch.open_uniform(d_bodies, stride, d_plain, plain_stride, count, n + 33, subkeys[0], c0 - 1, status)
     torch.cuda.synchronize()
     st = status.cpu().numpy().view(np.uint16)
-    plain = d_plain.cpu().numpy()
+    pall = d_pbuf.cpu().numpy()
+    plain = pall[pbase:]
+    if layout == "shift":
+        spans = [(pbase + i * plain_stride, pbase + i * plain_stride + n) for i in range(count)]
+        _gaps_untouched(pall, spans, 0, len(pall))
     fl = flags.cpu().numpy()
     for i in range(count):
         p = plain[i * plain_stride:i * plain_stride + n]

@@ -9,7 +9,8 @@ rc=$?; tail -2 gpurun_out/pytest_dense.log; [ $rc -eq 0 ] || { grep -E "^E |FAIL
 timeout -k 10 600 python -u -m pytest tests -m gpu -x -q --timeout 120 --timeout-method thread -p no:cacheprovider > gpurun_out/pytest_gpu.log 2>&1
 rc=$?; tail -2 gpurun_out/pytest_gpu.log; [ $rc -eq 0 ] || exit $rc
 for round in 1 2; do
-for a in "--out-stride 4129" "--out-stride 4136" "--out-stride 4224"; do
+IFS=";" read -ra AL <<< "${ARGS_LIST:---out-stride 4129;--out-stride 4136;--out-stride 4224}"
+for a in "${AL[@]}"; do
   for lib in "$@"; do
     CZ_LIB=$PWD/jeromq_amd/$lib timeout -k 10 200 python bench.py --config open4k --no-cpu-baseline --steps 20 --warmup 10 $a > gpurun_out/o.log 2>&1 || { tail gpurun_out/o.log; exit 3; }
     python -c "import json; d=json.loads(open('gpurun_out/o.log').read().strip().splitlines()[-1]); print('$lib $a round $round', d['value'], d['roofline']['kernel_ms'])"

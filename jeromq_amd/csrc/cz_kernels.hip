@@ -582,10 +582,42 @@ struct EmitRegion {
 // and the compiler's uniformity analysis moves everything that does not depend
 // on it -- 3 of the 4 first column quarter-rounds and 1 of the first row
 // quarter-rounds -- to the scalar unit (about 60 of the block's 960 VALU ops).
-template <int MODE, bool AL, class EM, bool PAIR = false, bool UN0 = false, bool LAZY = true>
-__device__ __forceinline__ void seal_frame(const uint8_t *__restrict__ in, u32 n, u32 flags, u64 counter,
+// INA (MODE_ZMQ): the payload's alignment class.  16: 16-byte aligned (AL as given); 8 / 1 (AL
+// true): payloads at 8-byte / any byte offsets (messages packed back to back), read from the
+// first dword boundary at or above the payload, `in + d` (d = -in & 3), with 16-byte loads.
+// The box funnel then shifts by sh = (in + 3) & 3 instead of 3, and the dword before the window,
+// P[-1] (flags << 24 for aligned payloads), holds the flags byte at byte sh and the first d
+// payload bytes above it.  Same VALU count as the aligned kernel.
+template <int MODE, bool AL, class EM, bool PAIR = false, bool UN0 = false, bool LAZY = true, int INA = 16>
+__device__ __forceinline__ void seal_frame(const uint8_t *__restrict__ in0, u32 n, u32 flags, u64 counter,
                                            const u32 key[8], EM &em)
 {
+    static_assert(INA == 16 || (MODE == MODE_ZMQ && AL), "INA 8/1: MESSAGE seal on the AL code paths");
+    const u32 ina_a = INA == 1 ? (u32)(uintptr_t)in0 & 3u : 0u;
+    const u32 ina_d = (4u - ina_a) & 3u;
+    const uint8_t *__restrict__ in = in0 + ina_d;  // dword-aligned for INA 8/1
+    const u32 sh = ina_a ? ina_a - 1u : 3u;
+    u32 pm1 = flags << 24;  // P[-1]
+    if constexpr (INA == 1) {
+        if (ina_a) {
+            const u32 r = *reinterpret_cast<const u32 *>(in0 - ina_a);
+            pm1 = (r & ~(0xffu << (8u * sh))) | (flags << (8u * sh));
+        }
+    }
+    auto ldF = [&](const uint8_t *p) -> V4 {  // all 16 bytes inside the payload
+        if constexpr (INA == 16) {
+            return ld16f<AL>(p);
+        } else {
+            const uint4 r = *reinterpret_cast<const u4_a4 *>(p);
+            return V4{r.x, r.y, r.z, r.w};
+        }
+    };
+    auto ldP = [&](const uint8_t *p, u64 avail) -> V4 {  // avail bytes inside the payload
+        if constexpr (INA == 16)
+            return ld16<AL>(p, avail);
+        else
+            return avail >= 16u ? ldF(p) : ld16<false>(p, avail);
+    };
     // ZMQ funnel: box dword k of block b = alignbyte(P[16b+k-8], P[16b+k-9], 3)
     // where P[i] is payload dword i; block b's window is P[16b-8 .. 16b+7]
     // (payload bytes [64b-32, 64b+32)) and P[16b-9] is carried from block b-1.
@@ -594,7 +626,7 @@ __device__ __forceinline__ void seal_frame(const uint8_t *__restrict__ in, u32 n
     const u32 mlen = (MODE == MODE_ZMQ || MODE == MODE_BOX) ? n + 33u : n;
     const u32 nfull = mlen >> 6;
     const u32 tailv = mlen & 63u;
-    const u64 inlen = MODE == MODE_BOX ? (u64)mlen : (u64)n;
+    const u64 inlen = MODE == MODE_BOX ? (u64)mlen : (u64)n - ina_d;  // bytes from `in`
     u32 n0, n1;
     counter_nonce(counter, n0, n1);
     if constexpr (UN0)
@@ -620,7 +652,7 @@ __device__ __forceinline__ void seal_frame(const uint8_t *__restrict__ in, u32 n
         ksblock(x, blk, 0u);
 #pragma unroll
         for (int k = 0; k < 16; k++)
-            C[k] = funnel(W[k + 1], W[k], 3) ^ x[k];
+            C[k] = funnel(W[k + 1], W[k], sh) ^ x[k];
         poly_block(P, C[0], C[1], C[2], C[3], 1u);
         poly_block(P, C[4], C[5], C[6], C[7], 1u);
         poly_block(P, C[8], C[9], C[10], C[11], 1u);
@@ -698,15 +730,15 @@ __device__ __forceinline__ void seal_frame(const uint8_t *__restrict__ in, u32 n
         u32 L[32];
 #pragma unroll
         for (int c = 0; c < 8; c++) {
-            V4 v = ld16<AL>(in + 16 * c, inlen > 16u * c ? inlen - 16u * c : 0);
+            V4 v = ldP(in + 16 * c, inlen > 16u * c ? inlen - 16u * c : 0);
             L[4 * c] = v.x; L[4 * c + 1] = v.y; L[4 * c + 2] = v.z; L[4 * c + 3] = v.w;
         }
         // block 0
         {
-            C[8] = funnel(L[0], flags << 24, 3) ^ x[8];
+            C[8] = funnel(L[0], pm1, sh) ^ x[8];
 #pragma unroll
             for (int k = 9; k < 16; k++)
-                C[k] = funnel(L[k - 8], L[k - 9], 3) ^ x[k];
+                C[k] = funnel(L[k - 8], L[k - 9], sh) ^ x[k];
             C[0] = HDR0; C[1] = HDR1; C[2] = n0; C[3] = n1;
             C[4] = C[5] = C[6] = C[7] = 0u;
             if (nfull >= 1) {
@@ -735,13 +767,13 @@ __device__ __forceinline__ void seal_frame(const uint8_t *__restrict__ in, u32 n
                 const u32 o = 128u * k;
 #pragma unroll
                 for (int c = 0; c < 6; c++) {
-                    V4 v = ld16f<AL>(src + 16 * c);
+                    V4 v = ldF(src + 16 * c);
                     L[4 * c] = v.x; L[4 * c + 1] = v.y; L[4 * c + 2] = v.z; L[4 * c + 3] = v.w;
                 }
 #pragma unroll
                 for (int c = 6; c < 8; c++) {
                     if (inlen > o + 16u * c) {
-                        V4 v = ld16f<AL>(src + 16 * c);
+                        V4 v = INA == 16 ? ld16f<AL>(src + 16 * c) : ldP(src + 16 * c, inlen - o - 16u * c);
                         L[4 * c] = v.x; L[4 * c + 1] = v.y; L[4 * c + 2] = v.z; L[4 * c + 3] = v.w;
                     }
                 }
@@ -774,12 +806,12 @@ __device__ __forceinline__ void seal_frame(const uint8_t *__restrict__ in, u32 n
         }
     } else {
         if constexpr (MODE == MODE_ZMQ) {
-            V4 a = ld16<AL>(in, inlen);
-            V4 b = ld16<AL>(in + 16, inlen > 16 ? inlen - 16 : 0);
-            u32 W[9] = {flags << 24, a.x, a.y, a.z, a.w, b.x, b.y, b.z, b.w};  // P[-1 .. 7]
+            V4 a = ldP(in, inlen);
+            V4 b = ldP(in + 16, inlen > 16 ? inlen - 16 : 0);
+            u32 W[9] = {pm1, a.x, a.y, a.z, a.w, b.x, b.y, b.z, b.w};  // P[-1 .. 7]
 #pragma unroll
             for (int k = 8; k < 16; k++)
-                C[k] = funnel(W[k - 7], W[k - 8], 3) ^ x[k];
+                C[k] = funnel(W[k - 7], W[k - 8], sh) ^ x[k];
             carry = b.w;
             C[0] = HDR0; C[1] = HDR1; C[2] = n0; C[3] = n1;
         } else {
@@ -818,10 +850,10 @@ __device__ __forceinline__ void seal_frame(const uint8_t *__restrict__ in, u32 n
         V4 q0, q1, q2, q3;
         if constexpr (MODE == MODE_ZMQ) {
             const uint8_t *src = in + 64u * blk - 32u;
-            q0 = ld16f<AL>(src);
-            q1 = ld16f<AL>(src + 16);
-            q2 = ld16f<AL>(src + 32);
-            q3 = ld16<AL>(src + 48, inlen - (64u * blk + 16u));  // may end inside this chunk
+            q0 = ldF(src);
+            q1 = ldF(src + 16);
+            q2 = ldF(src + 32);
+            q3 = ldP(src + 48, inlen - (64u * blk + 16u));  // may end inside this chunk
             u32 W[17] = {carry, q0.x, q0.y, q0.z, q0.w, q1.x, q1.y, q1.z, q1.w,
                          q2.x, q2.y, q2.z, q2.w, q3.x, q3.y, q3.z, q3.w};
             zmq_full_block(blk, W);
@@ -854,16 +886,16 @@ __device__ __forceinline__ void seal_frame(const uint8_t *__restrict__ in, u32 n
         for (int c = 0; c < 4; c++) {
             long o = (MODE == MODE_ZMQ) ? (long)(64u * blk) - 32 + 16 * c : (long)(64u * blk) + 16 * c;
             u64 avail = (o >= 0 && (u64)o < inlen) ? inlen - (u64)o : 0;
-            q[c] = ld16<AL>(in + o, avail);
+            q[c] = ldP(in + o, avail);
         }
         ksblock(x, blk, 0u);
         u32 W[16] = {q[0].x, q[0].y, q[0].z, q[0].w, q[1].x, q[1].y, q[1].z, q[1].w,
                      q[2].x, q[2].y, q[2].z, q[2].w, q[3].x, q[3].y, q[3].z, q[3].w};
         if constexpr (MODE == MODE_ZMQ) {
-            C[0] = funnel(W[0], carry, 3) ^ x[0];
+            C[0] = funnel(W[0], carry, sh) ^ x[0];
 #pragma unroll
             for (int k = 1; k < 16; k++)
-                C[k] = funnel(W[k], W[k - 1], 3) ^ x[k];
+                C[k] = funnel(W[k], W[k - 1], sh) ^ x[k];
         } else {
 #pragma unroll
             for (int k = 0; k < 16; k++)
@@ -2105,12 +2137,13 @@ enum Staging { ST_DIRECT = 0, ST_LINES = 1, ST_REGION = 2, ST_SHIFT = 3 };
 // a wave with fewer than 64 frames always stores directly.
 // MODE_BOX (cz_seal_uniform_box): frame i = the box at in + i*in_stride (len = payload bytes),
 // flags from box byte 32, flags8 unused.
-template <int ST, bool PAIR, int MODE = MODE_ZMQ>
-__global__ __launch_bounds__(BLOCK) CZ_OCC void k_seal_uniform(const uint8_t *__restrict__ in, uint64_t in_stride,
-                                                         uint8_t *__restrict__ out, uint64_t out_stride,
-                                                         uint32_t count, uint32_t len,
-                                                         const uint8_t *__restrict__ subkey, uint64_t counter0,
-                                                         const uint8_t *__restrict__ flags8, int allow_un0)
+// INA (seal_frame, MODE_ZMQ): 16 for 16-byte aligned payload slots; 8 / 1 for payloads at 8-byte /
+// any byte offsets (messages packed back to back), staged kernels only
+template <int ST, bool PAIR, int MODE, int INA>
+__device__ __forceinline__ void seal_uniform_body(const uint8_t *__restrict__ in, uint64_t in_stride,
+                                                  uint8_t *__restrict__ out, uint64_t out_stride, uint32_t count,
+                                                  uint32_t len, const uint8_t *__restrict__ subkey, uint64_t counter0,
+                                                  const uint8_t *__restrict__ flags8, int allow_un0)
 {
     extern __shared__ uint4 smem[];
     uint32_t i = blockIdx.x * BLOCK + threadIdx.x;
@@ -2139,9 +2172,9 @@ __global__ __launch_bounds__(BLOCK) CZ_OCC void k_seal_uniform(const uint8_t *__
                          dst, out_stride, lane, mlen, 0u, true,
                          smem + (WAVES * LINE_LDS_BYTES + (threadIdx.x >> 6) * HOLD_LDS_BYTES) / 16};
             if (un0)
-                seal_frame<MODE, true, EmitLines, PAIR, true>(src, len, fl, counter0 + i, key, em);
+                seal_frame<MODE, true, EmitLines, PAIR, true, true, INA>(src, len, fl, counter0 + i, key, em);
             else
-                seal_frame<MODE, true, EmitLines, PAIR, false>(src, len, fl, counter0 + i, key, em);
+                seal_frame<MODE, true, EmitLines, PAIR, false, true, INA>(src, len, fl, counter0 + i, key, em);
         } else if constexpr (ST == ST_SHIFT) {
             // bodies at any byte offset (dense packing, wire layout): byte-shifted line staging
             EmitShiftLinesUni em{reinterpret_cast<uint8_t *>(smem) + (threadIdx.x >> 6) * SHIFT_LDS_BYTES, dst, lane,
@@ -2149,17 +2182,17 @@ __global__ __launch_bounds__(BLOCK) CZ_OCC void k_seal_uniform(const uint8_t *__
             em.init(true);
             em.init_uniform(i - blockIdx.x * BLOCK, (u32)out_stride, out + (uint64_t)blockIdx.x * BLOCK * out_stride);
             if (un0)
-                seal_frame<MODE, true, EmitShiftLinesUni, PAIR, true>(src, len, fl, counter0 + i, key, em);
+                seal_frame<MODE, true, EmitShiftLinesUni, PAIR, true, true, INA>(src, len, fl, counter0 + i, key, em);
             else
-                seal_frame<MODE, true, EmitShiftLinesUni, PAIR, false>(src, len, fl, counter0 + i, key, em);
+                seal_frame<MODE, true, EmitShiftLinesUni, PAIR, false, true, INA>(src, len, fl, counter0 + i, key, em);
         } else {
             const u32 st = (u32)out_stride;
             EmitRegion em{smem + (threadIdx.x >> 6) * ((64u * st) >> 4), out + (uint64_t)wave_first * out_stride, st,
                           lane, mlen};
             if (un0)
-                seal_frame<MODE, true, EmitRegion, PAIR, true>(src, len, fl, counter0 + i, key, em);
+                seal_frame<MODE, true, EmitRegion, PAIR, true, true, INA>(src, len, fl, counter0 + i, key, em);
             else
-                seal_frame<MODE, true, EmitRegion, PAIR, false>(src, len, fl, counter0 + i, key, em);
+                seal_frame<MODE, true, EmitRegion, PAIR, false, true, INA>(src, len, fl, counter0 + i, key, em);
         }
         return;
     }
@@ -2176,6 +2209,29 @@ __global__ __launch_bounds__(BLOCK) CZ_OCC void k_seal_uniform(const uint8_t *__
         EmitDirect<false> em{dst, mlen};
         seal_frame<MODE, false>(src, len, fl, counter0 + i, key, em);
     }
+}
+
+template <int ST, bool PAIR, int MODE = MODE_ZMQ>
+__global__ __launch_bounds__(BLOCK) CZ_OCC void k_seal_uniform(const uint8_t *__restrict__ in, uint64_t in_stride,
+                                                         uint8_t *__restrict__ out, uint64_t out_stride,
+                                                         uint32_t count, uint32_t len,
+                                                         const uint8_t *__restrict__ subkey, uint64_t counter0,
+                                                         const uint8_t *__restrict__ flags8, int allow_un0)
+{
+    seal_uniform_body<ST, PAIR, MODE, 16>(in, in_stride, out, out_stride, count, len, subkey, counter0, flags8,
+                                          allow_un0);
+}
+
+// payloads off 16-byte alignment (INA 8 / 1): at least 3 waves per SIMD (uncapped, the funnelled
+// loads take the line kernels to 169-186 VGPRs, 2 waves)
+template <int ST, bool PAIR, int INA>
+__global__ __launch_bounds__(BLOCK) CZ_OCC CZ_OPEN_UNI_OCC void k_seal_uniform_ina(
+    const uint8_t *__restrict__ in, uint64_t in_stride, uint8_t *__restrict__ out, uint64_t out_stride, uint32_t count,
+    uint32_t len, const uint8_t *__restrict__ subkey, uint64_t counter0, const uint8_t *__restrict__ flags8,
+    int allow_un0)
+{
+    seal_uniform_body<ST, PAIR, MODE_ZMQ, INA>(in, in_stride, out, out_stride, count, len, subkey, counter0, flags8,
+                                               allow_un0);
 }
 
 __global__ __launch_bounds__(BLOCK) void k_seal_desc(const cz_frame_desc *__restrict__ desc,
@@ -3038,6 +3094,7 @@ static int g_un0 = 1;  // scalar first Salsa round when the high nonce word is w
 static int g_seglines = 1;  // line-staged stores for waves of equal-length segments
 static int g_shift = 1;     // uniform seal: shifted line staging for bodies at any byte offset
 static int g_open_ina = 1;  // uniform open: line path for bodies off 16-byte alignment (dword-aligned loads)
+static int g_seal_ina = 1;  // uniform seal: staged kernels for payloads off 16-byte alignment
 // segment kernels: waves of 16-byte aligned outputs that are not all on 128-byte lines go through
 // EmitShiftLines (whole cache lines) instead of EmitSegLines (128-byte groups at each output's
 // base, two partial cache lines per group): Zipf seal with 16-byte output slots 1250 -> 1629 GiB/s
@@ -3064,6 +3121,37 @@ hipError_t czk_seal_uniform(const void *in, uint64_t in_stride, void *out, uint6
 #define CZ_SEAL_LAUNCH(ST, PR, LDS)                                                                        \
     hipLaunchKernelGGL((k_seal_uniform<ST, PR>), grid, dim3(BLOCK), (LDS), s, (const uint8_t *)in, in_stride,   \
                        (uint8_t *)out, out_stride, count, len, (const uint8_t *)subkey, counter0, flags8, g_un0)
+    // payloads off 16-byte alignment (messages packed back to back): the staged kernels with
+    // dword-aligned loads (INA 8 / 1) instead of lane-wise unaligned loads and byte-exact stores
+    if (!in_al && g_pair && g_seal_ina && len >= 64u) {
+        const bool out_al = ((((uintptr_t)out | out_stride) & 15u) == 0);
+        int so = pick_staging(out_stride, len + 33u, out_al);
+        if (so == ST_DIRECT && len + 33u >= 256u && out_stride < (1ull << 22) && len < (1u << 29) && g_shift)
+            so = ST_SHIFT;
+        const bool i8 = (((uintptr_t)in | in_stride) & 7u) == 0;
+#define CZ_SEAL_LAUNCH_INA(ST, PR, INA, LDS)                                                                  \
+    hipLaunchKernelGGL((k_seal_uniform_ina<ST, PR, INA>), grid, dim3(BLOCK), (LDS), s, (const uint8_t *)in,        \
+                       in_stride, (uint8_t *)out, out_stride, count, len, (const uint8_t *)subkey, counter0,       \
+                       flags8, g_un0)
+        const unsigned lds_l = WAVES * (LINE_LDS_BYTES + HOLD_LDS_BYTES), lds_s = WAVES * SHIFT_LDS_BYTES;
+        const unsigned lds_r = (unsigned)(WAVES * 64 * out_stride);
+        if (so == ST_LINES) {
+            if (i8) CZ_SEAL_LAUNCH_INA(ST_LINES, true, 8, lds_l);
+            else CZ_SEAL_LAUNCH_INA(ST_LINES, true, 1, lds_l);
+            return hipGetLastError();
+        }
+        if (so == ST_SHIFT) {
+            if (i8) CZ_SEAL_LAUNCH_INA(ST_SHIFT, true, 8, lds_s);
+            else CZ_SEAL_LAUNCH_INA(ST_SHIFT, true, 1, lds_s);
+            return hipGetLastError();
+        }
+        if (so == ST_REGION) {
+            if (i8) CZ_SEAL_LAUNCH_INA(ST_REGION, false, 8, lds_r);
+            else CZ_SEAL_LAUNCH_INA(ST_REGION, false, 1, lds_r);
+            return hipGetLastError();
+        }
+#undef CZ_SEAL_LAUNCH_INA
+    }
     int st = pick_staging(out_stride, len + 33u, al);
     // bodies at any byte offset (dense slots, wire layout) from aligned payloads: shifted line staging
     // (EmitShiftLinesUni's buffer-store offsets, below 256 * stride + len + 160, stay below 2^31)
@@ -3294,6 +3382,11 @@ int czk_tune(const char *key, int value)
     if (__builtin_strcmp(key, "seglines") == 0) {
         int old = g_seglines;
         g_seglines = value != 0;
+        return old;
+    }
+    if (__builtin_strcmp(key, "seal_ina") == 0) {
+        int old = g_seal_ina;
+        g_seal_ina = value != 0;
         return old;
     }
     if (__builtin_strcmp(key, "open_ina") == 0) {

@@ -214,3 +214,33 @@ def test_open_uniform_any_offset(torch_dev, subkeys, n, stride, base, layout):
         else:
             assert st[i] & 0xff == _lib.CZ_STATUS_OK and st[i] >> 8 == fl[i], f"frame {i} status {st[i]:#x}"
             assert p.tobytes() == hin[i * in_stride:i * in_stride + n].tobytes(), f"frame {i} (stride {stride}, base {base})"
+
+
+@pytest.mark.parametrize("n,in_stride,out_stride", [(4096, 4097, 4224), (4096, 4100, 4224), (4096, 4104, 4224),
+                                                    (4096, 4097, 4129), (4096, 4104, 4136), (100, 100, 144),
+                                                    (100, 101, 144), (1000, 1003, 1041), (64, 65, 112)])
+@pytest.mark.parametrize("ibase", [0, 1, 3, 8])
+def test_seal_uniform_unaligned_payloads(torch_dev, subkeys, n, in_stride, out_stride, ibase):
+    """cz_seal_uniform of payloads packed at any byte offset (messages back to back in the caller's
+    buffer): the staged kernels with dword-aligned loads and a per-frame funnel shift, every body
+    against the oracle (CurveClientMechanism.encode), flags on some frames, the high nonce word
+    changing inside a wave, and a partial last wave."""
+    torch, dev = torch_dev
+    from jeromq_amd import batch
+    count = 64 * 5 + 17
+    hbuf = np.frombuffer(splitmix_bytes(ibase + count * in_stride + 64, 3000 + n + in_stride + ibase),
+                         dtype=np.uint8).copy()
+    d_buf = torch.from_numpy(hbuf).to(dev)
+    d_in = d_buf[ibase:]
+    d_out = torch.full((count * out_stride + 64,), SENTINEL, dtype=torch.uint8, device=dev)
+    flags = torch.tensor([(i % 3 == 0) | (2 if i % 7 == 0 else 0) for i in range(count)], dtype=torch.uint8, device=dev)
+    c0 = 0xFFFFFFF0 - 200
+    batch.seal_uniform(d_in, in_stride, d_out, out_stride, count, n, subkeys[0], c0, flags8=flags)
+    torch.cuda.synchronize()
+    out = d_out.cpu().numpy()
+    fl = flags.cpu().numpy()
+    for i in range(count):
+        p = hbuf[ibase + i * in_stride:ibase + i * in_stride + n].tobytes()
+        want = or_curve_encode(p, int(fl[i]), c0 + i, 0, PRECOM)
+        assert out[i * out_stride:i * out_stride + n + 33].tobytes() == want, \
+            f"frame {i} (in_stride {in_stride}, out_stride {out_stride}, ibase {ibase})"

@@ -1974,19 +1974,31 @@ __device__ __forceinline__ OpenSeg open_seg_geom(u32 size, u32 b0, u32 b1)
 
 // Open box blocks [b0, b1) of one MESSAGE body whose header passed open_header.
 // Returns CZ_STATUS_OK or (whole frame, bad tag) CZ_STATUS_CRYPTO.
-template <bool AL, class EM, bool AL8 = false>
+template <bool AL, class EM, bool AL8 = false, bool ANY = false>
 __device__ __forceinline__ u32 open_segment(const uint8_t *__restrict__ in, u32 size, const u32 key[8], u32 n0, u32 n1, u32 b0,
                             u32 b1, u32 *__restrict__ rec, u32 &flags_out, EM &em)
 {
-    // AL: input 16-byte aligned; AL8: 8-byte aligned (two 8-byte loads per chunk); else any
-    auto ldf = [&](const uint8_t *p) -> V4 {
-        if constexpr (AL8)
+    // AL: input 16-byte aligned; AL8: 8-byte aligned (two 8-byte loads per chunk); ANY: any byte
+    // offset (16-byte loads from the dword at or below, funnelled as open_frame's INA 1); else
+    // lane-wise unaligned loads
+    const u32 ina = ANY ? (u32)(uintptr_t)in & 3u : 0u;
+    const uint8_t *in4 = in - ina;
+    auto ldf = [&](const uint8_t *p) -> V4 {  // all 16 bytes inside the body
+        if constexpr (ANY) {
+            const uint8_t *q = in4 + (p - in);
+            const uint4 r = *reinterpret_cast<const u4_a4 *>(q);
+            const u32 r4 = ina ? *reinterpret_cast<const u32 *>(q + 16) : 0u;
+            return V4{funnel(r.y, r.x, ina), funnel(r.z, r.y, ina), funnel(r.w, r.z, ina), funnel(r4, r.w, ina)};
+        } else if constexpr (AL8) {
             return ld16f_8(p);
-        else
+        } else {
             return ld16f<AL>(p);
+        }
     };
     auto ldp = [&](const uint8_t *p, u64 avail) -> V4 {
-        if constexpr (AL8)
+        if constexpr (ANY)
+            return avail >= 16u ? ldf(p) : ld16<false>(p, avail);
+        else if constexpr (AL8)
             return ld16_8(p, avail);
         else
             return ld16<AL>(p, avail);
@@ -2422,6 +2434,7 @@ __device__ __forceinline__ bool wave_lines_ok(bool full_wave, u32 nchunks, bool 
 
 constexpr int SEGMODE_REST = 4;   // k_seal_segments: only the waves k_seal_segments_lines leaves
 constexpr int SEGMODE_SHIFT16 = 8;  // 16-byte aligned outputs not all on 128-byte lines: EmitShiftLines
+constexpr int SEGMODE_ANYIN = 16;   // open: bodies at any byte offset on the line path (funnelled loads)
 
 // Segment kernels.  With line staging and whole-line loads enabled the launcher runs two
 // kernels over the same segment list: k_seal_segments_lines takes every full wave of aligned
@@ -2607,8 +2620,9 @@ __global__ __launch_bounds__(BLOCK) CZ_OPEN_SEG_OCC void k_open_segments(const c
     // bodies at 8-byte offsets take the line emitters too, reading with 8-byte loads (lane-wise
     // byte-exact stores ran them at ~1030 GiB/s on the Zipf batch)
     const bool in_al8 = (((uintptr_t)src) & 7u) == 0;
+    const bool any_in = (mode & SEGMODE_ANYIN) != 0;  // bodies at any byte offset: funnelled loads
     u32 fl = 0;
-    if (allow_lines && wave_lines_ok(wave_first + 64u <= nseg, nch, in_al8) &&
+    if (allow_lines && wave_lines_ok(wave_first + 64u <= nseg, nch, in_al8 || any_in) &&
         __builtin_amdgcn_ballot_w64(early != CZ_STATUS_OK) == 0) {
         const u32 lane = threadIdx.x & 63u;
         uint8_t *wl = reinterpret_cast<uint8_t *>(smem) + (threadIdx.x >> 6) * SHIFT_LDS_BYTES;
@@ -2624,8 +2638,11 @@ __global__ __launch_bounds__(BLOCK) CZ_OPEN_SEG_OCC void k_open_segments(const c
             em.init(false);
             if (__builtin_amdgcn_ballot_w64(!in_al) == 0)
                 st = open_segment<true>(src, d.len, key, n0, n1, sg.first_block, b1, rec, fl, em);
-            else
+            else if (__builtin_amdgcn_ballot_w64(!in_al8) == 0)
                 st = open_segment<false, EmitShiftLines, true>(src, d.len, key, n0, n1, sg.first_block, b1, rec, fl, em);
+            else
+                st = open_segment<false, EmitShiftLines, false, true>(src, d.len, key, n0, n1, sg.first_block, b1, rec,
+                                                                      fl, em);
         }
         if (!rec)
             status[sg.frame] = (uint16_t)(st | (st == CZ_STATUS_OK ? (fl << 8) : 0u));
@@ -3348,7 +3365,8 @@ hipError_t czk_open_segments(const cz_frame_desc *desc, const cz_segment *segs, 
         hipLaunchKernelGGL(k_open_segments, dim3((nseg + BLOCK - 1) / BLOCK), dim3(BLOCK), WAVES * SHIFT_LDS_BYTES, s,
                            desc, segs, nseg, (const uint8_t *)in, (uint8_t *)out, (const uint8_t *)subkeys,
                            (u32 *)work, status, nonces,
-                           (g_seglines ? SEGMODE_LINES : 0) | (g_pair ? SEGMODE_PAIR : 0) | (g_shift16 ? SEGMODE_SHIFT16 : 0));
+                           (g_seglines ? SEGMODE_LINES : 0) | (g_pair ? SEGMODE_PAIR : 0) | (g_shift16 ? SEGMODE_SHIFT16 : 0) |
+                               (g_open_ina ? SEGMODE_ANYIN : 0));
     if (ncomb)
         hipLaunchKernelGGL(k_open_combine, dim3((ncomb + BLOCK - 1) / BLOCK), dim3(BLOCK), 0, s, desc, comb, ncomb,
                            (const uint8_t *)in, (uint8_t *)out, (const u32 *)work, status);

@@ -236,12 +236,13 @@ def test_zipf_seal_open_line_and_direct_stores(torch_dev, subkeys, L, seglines, 
         lib.cz_tune(b"pair", old_pair)
 
 
-@pytest.mark.parametrize("shift16", [1, 0])
-def test_zipf_open_8byte_bodies_and_16byte_outputs(torch_dev, subkeys, L, shift16):
+@pytest.mark.parametrize("shift16,pack", [(1, 8), (0, 8), (1, 1)])
+def test_zipf_open_8byte_bodies_and_16byte_outputs(torch_dev, subkeys, L, shift16, pack):
     """Line-emitter paths by alignment (cz_tune "shift16": 16-byte aligned outputs off the 128-byte
     lines through EmitShiftLines): a Zipf batch sealed into 16-byte slots vs the oracle, then its
-    bodies repacked at 8-byte offsets (the open's 8-byte-load lines path) and opened with tampered
-    and replayed frames mixed in; rejected frames leave zeros."""
+    bodies repacked at 8-byte offsets (the open's 8-byte-load lines path) or back to back (pack 1:
+    funnelled loads from any byte offset) and opened with tampered and replayed frames mixed in;
+    rejected frames leave zeros."""
     lib = L.lib()
     old = lib.cz_tune(b"shift16", shift16)
     try:
@@ -263,8 +264,8 @@ def test_zipf_open_8byte_bodies_and_16byte_outputs(torch_dev, subkeys, L, shift1
             b = bodies[i]
             b[int(rng.integers(16, len(b)))] ^= 0x04
             want[i] = L.CZ_STATUS_CRYPTO
-        odesc, ohin, oob = _bodies_desc(bodies, meta, pack=8)
-        assert (odesc["in_off"] % 16 == 8).any()
+        odesc, ohin, oob = _bodies_desc(bodies, meta, pack=pack)
+        assert (odesc["in_off"] % 16 == 8).any() if pack == 8 else (odesc["in_off"] % 4 == 3).any()
         for i in rng.choice(len(bodies), size=10, replace=False):
             if want[i] == L.CZ_STATUS_OK:
                 odesc[i]["counter"] = meta[i][2] + 1

@@ -1,6 +1,6 @@
 """In-process A/B of the segment kernels' SHIFT16 rule (cz_tune "shift16": 16-byte aligned outputs not
 on 128-byte lines through EmitShiftLines instead of EmitSegLines), seal and open of the Zipf batch.
-usage: python tools/dbg/seg_shift16_ab.py [out_align ...]"""
+usage: KNOB=shift16|open_ina python tools/dbg/seg_shift16_ab.py [out_align ...]"""
 import os, sys
 ROOT = os.path.join(os.path.dirname(os.path.abspath(__file__)), "..", "..")
 sys.path.insert(0, ROOT)
@@ -38,11 +38,11 @@ for oa in [int(x) for x in sys.argv[1:]] or [16, 8, 128]:
     op = lambda: batch.open_segments(d_odesc, oplan, wl.d_out, plain, wl.subkey.view(1, 32), status)
     for rnd in (1, 2):
         for v in (0, 1):
-            _lib.lib().cz_tune(b"shift16", v)
+            _lib.lib().cz_tune(os.environ.get("KNOB", "shift16").encode(), v)
             ts = timed(wl.step)
             to = timed(op)
             ok = bool(torch.equal(plain, wl.d_in)) and not bool((status & 0xff).any())
-            print(f"out_align {oa:3d} shift16={v} round {rnd}: seal {ts:.4f} ms {pay / ts * 1e3:7.1f} GiB/s | "
+            print(f"out_align {oa:3d} {os.environ.get('KNOB', 'shift16')}={v} round {rnd}: seal {ts:.4f} ms {pay / ts * 1e3:7.1f} GiB/s | "
                   f"open {to:.4f} ms {pay / to * 1e3:7.1f} GiB/s, plaintext ok {ok}", flush=True)
     del wl, plain
     torch.cuda.empty_cache()

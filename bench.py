@@ -55,7 +55,7 @@ def parse():
                     help="4k/100b/open4k: body slot stride in bytes (0 = the config's own layout)")
     ap.add_argument("--plain-stride", type=int, default=0,
                     help="open4k: plaintext slot stride in bytes (0 = the payload stride, 4096)")
-    ap.add_argument("--config", default="4k", choices=["4k", "4k_dense", "4k_box", "100b", "zipf", "zipf_lane", "open4k", "e2e4k",
+    ap.add_argument("--config", default="4k", choices=["4k", "4k_dense", "4k_box", "100b", "zipf", "zipf_open", "zipf_lane", "open4k", "e2e4k",
                                                           "engine", "nacl", "beforenm"])
     ap.add_argument("--frames", type=int, default=FRAMES)
     ap.add_argument("--chunk-frames", type=int, default=16384, help="e2e4k: frames per pipeline chunk")
@@ -122,7 +122,7 @@ def shard_plan(rank, frames_per_rank, cfg="4k"):
     """Rank r seals frames [r*F, (r+1)*F) of the global batch: nonce counters 3 + r*F ..,
     its own payload seed.  Frames are independent, so no data crosses ranks (weak scaling)."""
     counter0 = 3 + rank * frames_per_rank
-    seed = 0x5EED0000 + {"4k": 1, "4k_dense": 1, "4k_box": 1, "100b": 2, "zipf": 3, "zipf_lane": 3, "open4k": 4}[cfg] + 1000 * rank
+    seed = 0x5EED0000 + {"4k": 1, "4k_dense": 1, "4k_box": 1, "100b": 2, "zipf": 3, "zipf_open": 3, "zipf_lane": 3, "open4k": 4}[cfg] + 1000 * rank
     return counter0, seed
 
 
@@ -218,15 +218,31 @@ class Workload:
             self.d_desc = torch.from_numpy(desc.view(np.uint8)).to(dev)
             pay = int(lens.sum())
             self.payload_bytes = pay
-            if cfg == "zipf":
+            if cfg in ("zipf", "zipf_open"):
                 # long frames split into 64-block segments (one lane each) + Poly1305 combine
                 self.plan = batch.SegmentPlan(desc, open_=False, seg_blocks=seg_blocks).to(dev)
                 self.read_bytes = pay + 40 * frames + 16 * self.plan.nseg + 16 * self.plan.ncomb
+                if cfg == "zipf_open":
+                    # the receive side of the same batch: the sealed bodies at the output offset table
+                    # opened (tag check, replay floor, flags) into plaintext at the payload offsets
+                    batch.seal_segments(self.d_desc, self.plan, self.d_in, self.d_out, self.subkey.view(1, 32))
+                    odesc = desc.copy()
+                    odesc["in_off"], odesc["out_off"] = desc["out_off"], desc["in_off"]
+                    odesc["len"] = desc["len"] + np.uint64(33)
+                    odesc["counter"] = desc["counter"] - np.uint64(1)
+                    odesc["flags"] = 0x100  # CZ_DESC_CHECK_NONCE
+                    self.d_odesc = torch.from_numpy(odesc.view(np.uint8).copy()).to(dev)
+                    self.oplan = batch.SegmentPlan(odesc, open_=True, seg_blocks=seg_blocks).to(dev)
+                    self.d_plain = torch.empty_like(self.d_in)
+                    self.status = torch.empty(frames, dtype=torch.int16, device=dev)
+                    self.read_bytes = pay + 33 * frames + 40 * frames + 16 * self.oplan.nseg + 16 * self.oplan.ncomb
+                    self.write_bytes = pay + 2 * frames
             else:  # zipf_lane: one lane per frame, longest first
                 order = batch.plan_order(desc)
                 self.d_order = torch.from_numpy(order.view(np.int32)).to(dev)
                 self.read_bytes = pay + 40 * frames + 4 * frames
-            self.write_bytes = int((lens + np.uint64(33)).sum())
+            if cfg != "zipf_open":
+                self.write_bytes = int((lens + np.uint64(33)).sum())
             self.n = None
         torch.cuda.synchronize()
 
@@ -242,6 +258,9 @@ class Workload:
                                self.subkey, self.counter0 - 1, self.status)
         elif self.cfg == "zipf":
             batch.seal_segments(self.d_desc, self.plan, self.d_in, self.d_out, self.subkey.view(1, 32))
+        elif self.cfg == "zipf_open":
+            batch.open_segments(self.d_odesc, self.oplan, self.d_out, self.d_plain, self.subkey.view(1, 32),
+                                self.status)
         else:
             batch.seal_batch(self.d_desc, self.count, self.d_in, self.d_out, self.subkey.view(1, 32),
                              order=self.d_order)
@@ -259,6 +278,12 @@ class Workload:
                 fl = 1 if i % 8 == 0 else 0
                 if body != or_curve_encode(p, fl, self.counter0 + i, 0, PRECOM):
                     raise SystemExit(f"parity failure at frame {i}")
+        elif self.cfg == "zipf_open":
+            st = self.status.cpu().numpy().view(np.uint16)
+            if np.any(st & 0xff) or not np.array_equal(st >> 8, self.desc_np["flags"].astype(np.uint16)):
+                raise SystemExit("open failures in benchmark batch")
+            if not torch.equal(self.d_plain, self.d_in):  # payload lengths are 64-byte multiples: no padding
+                raise SystemExit("open round trip mismatch")
         elif self.cfg == "open4k":
             st = self.status.cpu().numpy().view(np.uint16)
             if np.any(st & 0xff):
@@ -899,6 +924,8 @@ def main():
                  "100b": "1M x 100 B frames, seal (configs[2])",
                  "zipf": "1M Zipf(1.2) 64 B..64 KiB frames, seal, segmented (configs[3])",
                  "zipf_lane": "1M Zipf(1.2) 64 B..64 KiB frames, seal, lane per frame (configs[3])",
+                 "zipf_open": "1M Zipf(1.2) 64 B..64 KiB frames, open+verify of the sealed batch, segmented "
+                              "(configs[3], receive side)",
                  "open4k": "1M x 4 KiB frames, open+verify (configs[4] leg)"}
         line = {
             "metric": "CURVE encrypt+MAC GiB/s (device-resident), batched 4 KiB frames, 1/2/4/8 GPU",

@@ -18,6 +18,7 @@ sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
 from pmc_key import file_safe, parse  # noqa: E402
 KERNELS = {"4k": ("k_seal_uniform",), "100b": ("k_seal_uniform",), "open4k": ("k_open_uniform",),
            "zipf": ("k_seal_segments", "k_seal_combine"), "zipf_lane": ("k_seal_desc",),
+           "zipf_open": ("k_open_segments", "k_open_combine"),
            "4k_dense": ("k_seal_uniform",)}
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 path = os.path.join(ROOT, "profiles", "pmc_traffic.json")

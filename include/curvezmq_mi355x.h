@@ -77,7 +77,10 @@ extern "C" {
 
 /*
  * One frame of a batch (40 bytes).  Offsets are byte offsets into the batch's
- * in / out buffers; 16-byte aligned offsets take the vectorised fast path.
+ * in / out buffers, any alignment.  The segment kernels store outputs at any byte offset
+ * through line staging (whole 128-byte cache lines); the open reads bodies at any byte
+ * offset with dword-aligned loads; the seal's fast path reads 16-byte aligned payloads
+ * (others run lane-wise).
  *   seal: in  = payload (len = n bytes)      out = MESSAGE body (n + 33 bytes)
  *         counter = the 8-byte nonce counter (cnNonce), flags low byte = MORE|COMMAND
  *   open: in  = MESSAGE body (len = size)    out = payload (size - 33 bytes)
@@ -134,10 +137,12 @@ int cz_open_batch(const cz_frame_desc *d_desc, const uint32_t *d_order, uint32_t
 
 /* Uniform-length batch of ONE connection direction: frame i at in + i*in_stride,
  * body i at out + i*out_stride, nonce counter0 + i, flags d_flags8[i] (NULL = 0).
- * The batch owns count * out_stride output bytes: slot bytes past a body are
- * written as zero (this lets the kernel store whole 128-byte lines; an
- * out_stride that is a multiple of 128 -- or 64 slots <= 16 KiB -- takes the
- * LDS-staged full-line store path). */
+ * Any strides and base alignments: payloads packed at any byte offset are read with
+ * dword-aligned loads; an out_stride that is a multiple of 128 (or 64 slots <= 16 KiB)
+ * makes the batch own count * out_stride output bytes, and slot bytes past a body are
+ * written as zero (whole 128-byte lines stored once); any other out_stride (e.g. bodies
+ * back to back, 4129 bytes apart at 4 KiB) goes through byte-shifted line staging and
+ * leaves the bytes between bodies as the caller wrote them. */
 int cz_seal_uniform(uint32_t count, uint32_t len, const void *d_in, uint64_t in_stride, void *d_out,
                     uint64_t out_stride, const void *d_subkey, uint64_t counter0, const uint8_t *d_flags8,
                     void *stream);
@@ -150,8 +155,11 @@ int cz_seal_uniform_box(uint32_t count, uint32_t len, const void *d_box, uint64_
                         uint64_t out_stride, const void *d_subkey, uint64_t counter0, void *stream);
 /* Open `count` bodies of `size` bytes of one connection in order; frame 0 must
  * beat floor0, frame i must beat frame i-1 (when check != 0).  Payload i goes to
- * out + i*out_stride; the batch owns count * out_stride output bytes (slot bytes
- * past a payload, and rejected frames' slots, are written as zero). */
+ * out + i*out_stride.  Bodies at any byte offset (in_stride 4129: the dense wire
+ * layout) are read with dword-aligned loads.  out_stride a multiple of 128: the batch
+ * owns count * out_stride output bytes (slot bytes past a payload, and rejected frames'
+ * slots, are written as zero); any other out_stride: byte-shifted line staging, bytes
+ * between payloads untouched, rejected frames' payload bytes written as zero. */
 int cz_open_uniform(uint32_t count, uint32_t size, const void *d_in, uint64_t in_stride, void *d_out,
                     uint64_t out_stride, const void *d_subkey, uint64_t floor0, int check, uint16_t *d_status,
                     void *stream);
@@ -427,7 +435,12 @@ int cz_device_ok(void);
 /* Kernel-variant knob for A/B measurement; returns the previous value or CZ_EINVAL.
  *   "pair": 1 = seal kernels read whole 128-byte input lines per two blocks (default), 0 = per block
  *   "un0":  1 = scalar first Salsa round when the high nonce word is wave-uniform (default), 0 = off
- *   "seglines": 1 = line-staged stores in the segment kernels (default), 0 = direct stores */
+ *   "seglines": 1 = line-staged stores in the segment kernels (default), 0 = direct stores
+ *   "shift": 1 = byte-shifted line staging for uniform outputs off 128-byte slots (default)
+ *   "shift16": 1 = segment outputs that are 16-byte but not 128-byte aligned through the
+ *              byte-shifted line emitter (default), 0 = 128-byte groups at each output's base
+ *   "open_ina" / "seal_ina": 1 = line paths for bodies / payloads off 16-byte alignment with
+ *              dword-aligned loads (default), 0 = lane-wise unaligned paths */
 int cz_tune(const char *key, int value);
 
 #ifdef __cplusplus

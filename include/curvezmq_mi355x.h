@@ -78,9 +78,8 @@ extern "C" {
 /*
  * One frame of a batch (40 bytes).  Offsets are byte offsets into the batch's
  * in / out buffers, any alignment.  The segment kernels store outputs at any byte offset
- * through line staging (whole 128-byte cache lines); the open reads bodies at any byte
- * offset with dword-aligned loads; the seal's fast path reads 16-byte aligned payloads
- * (others run lane-wise).
+ * through line staging (whole 128-byte cache lines) and read payloads / bodies at any byte
+ * offset with dword-aligned loads (16-byte aligned inputs are fastest).
  *   seal: in  = payload (len = n bytes)      out = MESSAGE body (n + 33 bytes)
  *         counter = the 8-byte nonce counter (cnNonce), flags low byte = MORE|COMMAND
  *   open: in  = MESSAGE body (len = size)    out = payload (size - 33 bytes)

@@ -1748,16 +1748,44 @@ __device__ __forceinline__ u32 seal_seg_bytes(u32 mlen, u32 b0, u32 bend)
 // whole (8 back-to-back loads) and seals two blocks from it, carrying the
 // line's last 9 dwords.  Lane-wise 16-byte loads one block apart made L2 fetch
 // most lines twice (2.6x the payload on the Zipf batch).
-template <bool AL, class EM, bool PAIR = false>
-__device__ __forceinline__ void seal_segment(const uint8_t *__restrict__ in, u32 n, u32 flags, u64 counter, const u32 key[8], u32 b0,
+// INA: as seal_frame's (16: 16-byte aligned payload; 8 / 1 with AL true: payload at an 8-byte /
+// any byte offset, read from the dword boundary at or above it with the funnel shift sh).
+template <bool AL, class EM, bool PAIR = false, int INA = 16>
+__device__ __forceinline__ void seal_segment(const uint8_t *__restrict__ in0, u32 n, u32 flags, u64 counter, const u32 key[8], u32 b0,
                              u32 b1, u32 *__restrict__ rec, EM &em, u32 nrun = 0)
 {
+    static_assert(INA == 16 || AL, "INA 8/1 take the AL code paths");
+    const u32 ina_a = INA == 1 ? (u32)(uintptr_t)in0 & 3u : 0u;
+    const u32 ina_d = (4u - ina_a) & 3u;
+    const uint8_t *__restrict__ in = in0 + ina_d;
+    const u32 sh = ina_a ? ina_a - 1u : 3u;
+    u32 pm1 = flags << 24;  // P[-1]
+    if constexpr (INA == 1) {
+        if (ina_a) {
+            const u32 r = *reinterpret_cast<const u32 *>(in0 - ina_a);
+            pm1 = (r & ~(0xffu << (8u * sh))) | (flags << (8u * sh));
+        }
+    }
+    auto ldF = [&](const uint8_t *p) -> V4 {
+        if constexpr (INA == 16) {
+            return ld16f<AL>(p);
+        } else {
+            const uint4 r = *reinterpret_cast<const u4_a4 *>(p);
+            return V4{r.x, r.y, r.z, r.w};
+        }
+    };
+    auto ldP = [&](const uint8_t *p, u64 avail) -> V4 {
+        if constexpr (INA == 16)
+            return ld16<AL>(p, avail);
+        else
+            return avail >= 16u ? ldF(p) : ld16<false>(p, avail);
+    };
     const u32 mlen = n + 33u;
     const u32 nblk = (mlen + 63u) >> 6;
     const u32 nfull = mlen >> 6;
     const u32 bend = b1 < nblk ? b1 : nblk;
     const u32 nch = bend - b0;
-    const u64 inlen = n;
+    const u64 inlen = (u64)n - ina_d;  // bytes from `in`
     u32 n0, n1;
     counter_nonce(counter, n0, n1);
     u32 x[16], C[16];
@@ -1773,7 +1801,7 @@ __device__ __forceinline__ void seal_segment(const uint8_t *__restrict__ in, u32
         salsa20_block(x, key, n0, n1, blk, 0u);
 #pragma unroll
         for (int k = 0; k < 16; k++)
-            C[k] = funnel(W[k + 1], W[k], 3) ^ x[k];
+            C[k] = funnel(W[k + 1], W[k], sh) ^ x[k];
         if (blk == 0) {
             C[0] = HDR0; C[1] = HDR1; C[2] = n0; C[3] = n1;
             C[4] = C[5] = C[6] = C[7] = 0u;  // tag slot
@@ -1822,11 +1850,11 @@ __device__ __forceinline__ void seal_segment(const uint8_t *__restrict__ in, u32
 #pragma unroll
             for (int c = 0; c < 8; c++) {
                 const long o = (long)(64u * b0) - 64 + 16 * c;
-                V4 v = (o < 0) ? zero4() : ld16<AL>(ln + 16 * c, (u64)o < inlen ? inlen - (u64)o : 0);
+                V4 v = (o < 0) ? zero4() : ldP(ln + 16 * c, (u64)o < inlen ? inlen - (u64)o : 0);
                 L[4 * c] = v.x; L[4 * c + 1] = v.y; L[4 * c + 2] = v.z; L[4 * c + 3] = v.w;
             }
             if (b0 == 0)
-                L[15] = flags << 24;  // P[-1]
+                L[15] = pm1;  // P[-1]
             block(b0, L + 7, 0u < nch);
             em.emit(0u, C);
 #pragma unroll
@@ -1837,10 +1865,10 @@ __device__ __forceinline__ void seal_segment(const uint8_t *__restrict__ in, u32
 #pragma unroll
             for (int k = 0; k < 8; k++)
                 cy[k] = 0u;
-            cy[8] = flags << 24;
+            cy[8] = pm1;
         } else {
             const uint8_t *p = in + 64u * b0 - 48u;
-            V4 a = ld16f<AL>(p), b = ld16f<AL>(p + 16), c = ld16f<AL>(p + 32);
+            V4 a = ldF(p), b = ldF(p + 16), c = ldF(p + 32);
             cy[0] = a.w; cy[1] = b.x; cy[2] = b.y; cy[3] = b.z; cy[4] = b.w;
             cy[5] = c.x; cy[6] = c.y; cy[7] = c.z; cy[8] = c.w;
         }
@@ -1852,13 +1880,13 @@ __device__ __forceinline__ void seal_segment(const uint8_t *__restrict__ in, u32
             if (o + 128u <= inlen) {
 #pragma unroll
                 for (int c = 0; c < 8; c++) {
-                    V4 v = ld16f<AL>(src + 16 * c);
+                    V4 v = ldF(src + 16 * c);
                     L[4 * c] = v.x; L[4 * c + 1] = v.y; L[4 * c + 2] = v.z; L[4 * c + 3] = v.w;
                 }
             } else {
 #pragma unroll
                 for (int c = 0; c < 8; c++) {
-                    V4 v = ld16<AL>(src + 16 * c, inlen > o + 16u * c ? inlen - o - 16u * c : 0);
+                    V4 v = ldP(src + 16 * c, inlen > o + 16u * c ? inlen - o - 16u * c : 0);
                     L[4 * c] = v.x; L[4 * c + 1] = v.y; L[4 * c + 2] = v.z; L[4 * c + 3] = v.w;
                 }
             }
@@ -1880,14 +1908,14 @@ __device__ __forceinline__ void seal_segment(const uint8_t *__restrict__ in, u32
                 cy[k] = L[23 + k];
         }
     } else {
-        u32 carry = b0 == 0 ? (flags << 24) : ld32<AL>(in + 64u * b0 - 36u);  // P[16*b0 - 9]
+        u32 carry = b0 == 0 ? pm1 : (INA == 16 ? ld32<AL>(in + 64u * b0 - 36u) : *reinterpret_cast<const u32 *>(in + 64u * b0 - 36u));  // P[16*b0 - 9]
         for (u32 q = 0; q < nch; q++) {
             const u32 blk = b0 + q;
             u32 W[17];
             W[0] = carry;
             if (blk == 0) {
-                V4 a = ld16<AL>(in, inlen);
-                V4 b = ld16<AL>(in + 16, inlen > 16 ? inlen - 16 : 0);
+                V4 a = ldP(in, inlen);
+                V4 b = ldP(in + 16, inlen > 16 ? inlen - 16 : 0);
                 // block 0 only uses W[8..16] = P[-1 .. 7]
                 W[8] = carry;
                 W[9] = a.x; W[10] = a.y; W[11] = a.z; W[12] = a.w;
@@ -1899,14 +1927,14 @@ __device__ __forceinline__ void seal_segment(const uint8_t *__restrict__ in, u32
                 const uint8_t *src = in + 64u * blk - 32u;
                 V4 q0, q1, q2, q3;
                 if (blk < nfull) {
-                    q0 = ld16f<AL>(src); q1 = ld16f<AL>(src + 16); q2 = ld16f<AL>(src + 32);
-                    q3 = ld16<AL>(src + 48, inlen - (64u * blk + 16u));
+                    q0 = ldF(src); q1 = ldF(src + 16); q2 = ldF(src + 32);
+                    q3 = ldP(src + 48, inlen - (64u * blk + 16u));
                 } else {
                     const u64 o = 64u * blk - 32u;
-                    q0 = ld16<AL>(src, o < inlen ? inlen - o : 0);
-                    q1 = ld16<AL>(src + 16, o + 16 < inlen ? inlen - o - 16 : 0);
-                    q2 = ld16<AL>(src + 32, o + 32 < inlen ? inlen - o - 32 : 0);
-                    q3 = ld16<AL>(src + 48, o + 48 < inlen ? inlen - o - 48 : 0);
+                    q0 = ldP(src, o < inlen ? inlen - o : 0);
+                    q1 = ldP(src + 16, o + 16 < inlen ? inlen - o - 16 : 0);
+                    q2 = ldP(src + 32, o + 32 < inlen ? inlen - o - 32 : 0);
+                    q3 = ldP(src + 48, o + 48 < inlen ? inlen - o - 48 : 0);
                 }
                 W[1] = q0.x; W[2] = q0.y; W[3] = q0.z; W[4] = q0.w;
                 W[5] = q1.x; W[6] = q1.y; W[7] = q1.z; W[8] = q1.w;
@@ -2434,7 +2462,7 @@ __device__ __forceinline__ bool wave_lines_ok(bool full_wave, u32 nchunks, bool 
 
 constexpr int SEGMODE_REST = 4;   // k_seal_segments: only the waves k_seal_segments_lines leaves
 constexpr int SEGMODE_SHIFT16 = 8;  // 16-byte aligned outputs not all on 128-byte lines: EmitShiftLines
-constexpr int SEGMODE_ANYIN = 16;   // open: bodies at any byte offset on the line path (funnelled loads)
+constexpr int SEGMODE_ANYIN = 16;   // inputs at any byte offset on the line paths (dword-aligned loads)
 
 // Segment kernels.  With line staging and whole-line loads enabled the launcher runs two
 // kernels over the same segment list: k_seal_segments_lines takes every full wave of aligned
@@ -2509,6 +2537,23 @@ __device__ __forceinline__ void seal_segments_body(const cz_frame_desc *__restri
                 em.init(sg.first_block == 0);
                 seal_segment<true>(src, d.len, d.flags & 0xffu, d.counter, key, sg.first_block, b1, rec, em);
             }
+            return;
+        }
+    }
+    if constexpr (PART == SEGPART_REST) {
+        // full waves left here because some payload is off 16-byte alignment: line-staged stores
+        // with dword-aligned loads (seal_segment INA 8 / 1) instead of lane-wise paths
+        if (allow_lines && pair && full_wave && (mode & SEGMODE_ANYIN)) {
+            const u32 lane = threadIdx.x & 63u;
+            uint8_t *wl = reinterpret_cast<uint8_t *>(smem) + (threadIdx.x >> 6) * SHIFT_LDS_BYTES;
+            EmitShiftLines em{wl, dst, lane, total, 0u, 0u};
+            em.init(sg.first_block == 0);
+            if (__builtin_amdgcn_ballot_w64((((uintptr_t)src) & 7u) != 0u) == 0)
+                seal_segment<true, EmitShiftLines, true, 8>(src, d.len, d.flags & 0xffu, d.counter, key,
+                                                            sg.first_block, b1, rec, em, wave_max(nch));
+            else
+                seal_segment<true, EmitShiftLines, true, 1>(src, d.len, d.flags & 0xffu, d.counter, key,
+                                                            sg.first_block, b1, rec, em, wave_max(nch));
             return;
         }
     }
@@ -3111,7 +3156,7 @@ static int g_un0 = 1;  // scalar first Salsa round when the high nonce word is w
 static int g_seglines = 1;  // line-staged stores for waves of equal-length segments
 static int g_shift = 1;     // uniform seal: shifted line staging for bodies at any byte offset
 static int g_open_ina = 1;  // uniform open: line path for bodies off 16-byte alignment (dword-aligned loads)
-static int g_seal_ina = 1;  // uniform seal: staged kernels for payloads off 16-byte alignment
+static int g_seal_ina = 1;  // seal: staged / line paths for payloads off 16-byte alignment
 // segment kernels: waves of 16-byte aligned outputs that are not all on 128-byte lines go through
 // EmitShiftLines (whole cache lines) instead of EmitSegLines (128-byte groups at each output's
 // base, two partial cache lines per group): Zipf seal with 16-byte output slots 1250 -> 1629 GiB/s
@@ -3341,11 +3386,12 @@ hipError_t czk_seal_segments(const cz_frame_desc *desc, const cz_segment *segs, 
 #else
     if (nseg && g_seglines && g_pair) {
 #endif
-        const int mode = SEGMODE_LINES | SEGMODE_PAIR | (g_shift16 ? SEGMODE_SHIFT16 : 0);
+        const int mode = SEGMODE_LINES | SEGMODE_PAIR | (g_shift16 ? SEGMODE_SHIFT16 : 0) | (g_seal_ina ? SEGMODE_ANYIN : 0);
         hipLaunchKernelGGL(k_seal_segments_lines, grid, dim3(BLOCK), WAVES * SHIFT_LDS_BYTES, s, desc, segs, nseg,
                            (const uint8_t *)in, (uint8_t *)out, (const uint8_t *)subkeys, (u32 *)work, mode);
-        hipLaunchKernelGGL(k_seal_segments, grid, dim3(BLOCK), 0, s, desc, segs, nseg, (const uint8_t *)in,
-                           (uint8_t *)out, (const uint8_t *)subkeys, (u32 *)work, mode | SEGMODE_REST);
+        hipLaunchKernelGGL(k_seal_segments, grid, dim3(BLOCK), g_seal_ina ? WAVES * SHIFT_LDS_BYTES : 0, s, desc, segs,
+                           nseg, (const uint8_t *)in, (uint8_t *)out, (const uint8_t *)subkeys, (u32 *)work,
+                           mode | SEGMODE_REST);
     } else if (nseg) {
         hipLaunchKernelGGL(k_seal_segments, grid, dim3(BLOCK), WAVES * SHIFT_LDS_BYTES, s, desc, segs, nseg,
                            (const uint8_t *)in, (uint8_t *)out, (const uint8_t *)subkeys, (u32 *)work,

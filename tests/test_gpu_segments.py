@@ -341,3 +341,35 @@ def test_full_size_zipf_roundtrip(torch_dev, subkeys, L):
     assert oracle_check_full(d_in, d_out, desc, PRECOM) == n
     del d_in, d_out, d_plain
     torch.cuda.empty_cache()
+
+
+@pytest.mark.parametrize("in_round,out_round", [(1, 16), (8, 8), (1, 1)])
+def test_zipf_seal_payloads_at_any_offset(torch_dev, subkeys, L, in_round, out_round):
+    """Ragged payloads packed at 1- or 8-byte granularity (messages back to back in the caller's
+    buffer): full waves take the line-staged path with dword-aligned loads and the per-frame funnel
+    (cz_tune "seal_ina"); every body against the oracle, with both settings of the knob."""
+    torch, dev = torch_dev
+    rng = np.random.default_rng(31 + in_round + out_round)
+    j = np.clip(rng.zipf(1.2, size=3000), 1, 1024)
+    lens = [int(x) for x in (64 * j - rng.integers(0, 64, size=len(j)))]
+    desc = np.zeros(len(lens), dtype=DESC_DTYPE)
+    io = oo = 0
+    for i, n in enumerate(lens):
+        desc[i] = (io, oo, n, 0, 7 + 3 * i, i & 3, -1)
+        io += (n + in_round - 1) // in_round * in_round
+        oo += (n + 33 + out_round - 1) // out_round * out_round
+    assert (desc["in_off"] % 16 != 0).sum() > len(lens) // 3
+    hin = np.frombuffer(splitmix_bytes(io + 64, 41 + in_round), dtype=np.uint8).copy()
+    ob = oo + 64
+    want = _oracle_seal(desc, hin, ob)
+    lib = L.lib()
+    old = lib.cz_tune(b"seal_ina", 1)
+    try:
+        for v in (1, 0):
+            lib.cz_tune(b"seal_ina", v)
+            out, plan = _seal_seg(torch_dev, subkeys, desc, hin, ob, 64)
+            assert plan.ncomb > 0
+            bad = np.nonzero(out != want)[0]
+            assert bad.size == 0, f"seal_ina={v}: {bad.size} bytes differ, first at {int(bad[0])}"
+    finally:
+        lib.cz_tune(b"seal_ina", old)

@@ -2348,7 +2348,7 @@ __global__ __launch_bounds__(BLOCK) CZ_OCC CZ_OPEN_UNI_OCC void k_open_uniform(c
                                                          const uint8_t *__restrict__ subkey, uint64_t floor0,
                                                          int check, uint16_t *__restrict__ status, int allow_un0)
 {
-    static_assert(INA == 16 || ST == ST_LINES || ST == ST_SHIFT, "unaligned bodies: line-staged plaintext only");
+    static_assert(INA == 16 || ST != ST_DIRECT, "unaligned bodies: staged plaintext only");
     extern __shared__ uint4 smem[];
     uint32_t i = blockIdx.x * BLOCK + threadIdx.x;
     if constexpr (ST == ST_SHIFT) {
@@ -2402,16 +2402,16 @@ __global__ __launch_bounds__(BLOCK) CZ_OCC CZ_OPEN_UNI_OCC void k_open_uniform(c
             else
                 st = open_frame<MODE_ZMQ, true, EmitShiftLinesUni, PAIR, false, true, INA>(src, size, key, check != 0,
                                                                                           floor, &fl, &nonce, 0, em);
-        } else if constexpr (INA == 16) {
+        } else {
             const u32 ost = (u32)out_stride;
             EmitRegion em{smem + (threadIdx.x >> 6) * ((64u * ost) >> 4), out + (uint64_t)wave_first * out_stride,
                           ost, lane, nout};
             if (un0)
-                st = open_frame<MODE_ZMQ, true, EmitRegion, PAIR, true>(src, size, key, check != 0, floor, &fl, &nonce,
-                                                                       0, em);
+                st = open_frame<MODE_ZMQ, true, EmitRegion, PAIR, true, true, INA>(src, size, key, check != 0, floor,
+                                                                                  &fl, &nonce, 0, em);
             else
-                st = open_frame<MODE_ZMQ, true, EmitRegion, PAIR, false>(src, size, key, check != 0, floor, &fl,
-                                                                        &nonce, 0, em);
+                st = open_frame<MODE_ZMQ, true, EmitRegion, PAIR, false, true, INA>(src, size, key, check != 0, floor,
+                                                                                   &fl, &nonce, 0, em);
         }
         // rejected frames ran the loop as dead lanes: their slots hold zeros
         status[i] = (uint16_t)(st | (st == CZ_STATUS_OK ? (fl << 8) : 0u));
@@ -3309,6 +3309,19 @@ hipError_t czk_open_uniform(const void *in, uint64_t in_stride, void *out, uint6
         st_out = ST_SHIFT;
     const uint64_t ia = (uintptr_t)in | in_stride;
     const int ina = (ia & 15u) == 0 ? 16 : (ia & 7u) == 0 ? 8 : 1;
+    const unsigned lds_out_region = (unsigned)(WAVES * 64 * out_stride);
+    if (ina != 16 && st_out == ST_REGION && g_open_ina) {
+        // small bodies (64 plaintext slots <= 16 KiB) off 16-byte alignment: region staging
+        if (ina == 8)
+            hipLaunchKernelGGL((k_open_uniform<ST_REGION, false, 8>), grid, dim3(BLOCK), lds_out_region, s,
+                               (const uint8_t *)in, in_stride, (uint8_t *)out, out_stride, count, size,
+                               (const uint8_t *)subkey, floor0, check, status, g_un0);
+        else
+            hipLaunchKernelGGL((k_open_uniform<ST_REGION, false, 1>), grid, dim3(BLOCK), lds_out_region, s,
+                               (const uint8_t *)in, in_stride, (uint8_t *)out, out_stride, count, size,
+                               (const uint8_t *)subkey, floor0, check, status, g_un0);
+        return hipGetLastError();
+    }
     if (g_pair && (st_out == ST_SHIFT || (st_out == ST_LINES && ina != 16)) && (ina == 16 || g_open_ina)) {
         if (st_out == ST_LINES) {
             if (ina == 8)

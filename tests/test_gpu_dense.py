@@ -160,7 +160,7 @@ def test_open_segments_dense_plaintext(torch_dev, subkeys, out_round):
 
 
 @pytest.mark.parametrize("n,stride", [(4096, 4129), (4096, 4130), (4096, 4131), (4096, 4136), (4096, 4144),
-                                      (300, 333), (1000, 1041)])
+                                      (300, 333), (1000, 1041), (100, 133), (100, 136)])
 @pytest.mark.parametrize("base", [0, 1, 8, 13])
 @pytest.mark.parametrize("layout", ["line", "shift"])
 def test_open_uniform_any_offset(torch_dev, subkeys, n, stride, base, layout):

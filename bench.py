@@ -70,22 +70,77 @@ def parse():
     return ap.parse_args()
 
 
+def _free_port():
+    import socket
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    return port
+
+
+def launch_ranks(gpus, argv, popen=None):
+    """`python bench.py --gpus N` with N > 1 and no launcher around it: start the N ranks as a CHILD
+    `torch.distributed.run` (one process per GPU, rendezvous on 127.0.0.1), relay rank 0's JSON
+    line and return the child's exit status.  This process never touches the GPU (torch.cuda stays
+    uninitialised, the library is not loaded) and never execs: the ranks are its children.  The
+    line is checked before it is relayed: exactly one JSON line, n_gpus == N, one per_rank entry per
+    rank; anything else is an error (exit 1), so a run that silently timed fewer GPUs cannot pass."""
+    import subprocess
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={gpus}",
+           "--master-addr", "127.0.0.1", "--master-port", str(_free_port()), os.path.abspath(__file__)] + list(argv)
+    env = dict(os.environ)
+    env.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")  # dmabuf IPC: RCCL needs it on this pool
+    print("launching: " + " ".join(cmd), file=sys.stderr, flush=True)
+    p = (popen or subprocess.Popen)(cmd, stdout=subprocess.PIPE, text=True, env=env, cwd=ROOT)
+    lines = []
+    for ln in p.stdout:   # ranks' other stdout goes to stderr; the JSON line is held for the check
+        if ln.startswith("{"):
+            lines.append(ln.strip())
+        else:
+            sys.stderr.write(ln)
+            sys.stderr.flush()
+    rc = p.wait()
+    assert not torch.cuda.is_initialized(), "launcher process initialised the GPU"
+    if rc != 0:
+        print(f"bench ranks failed (exit {rc})", file=sys.stderr)
+        return rc
+    if len(lines) != 1:
+        print(f"expected one JSON line from rank 0, got {len(lines)}", file=sys.stderr)
+        return 1
+    line = json.loads(lines[0])
+    per = line.get("per_rank") or []
+    if line.get("n_gpus") != gpus or len(per) != gpus or sorted(r["rank"] for r in per) != list(range(gpus)):
+        print(f"rank line does not cover {gpus} GPUs: n_gpus={line.get('n_gpus')}, per_rank={len(per)}",
+              file=sys.stderr)
+        return 1
+    line["launcher"] = "bench.py --gpus: child torch.distributed.run"
+    print(json.dumps(line), flush=True)
+    return 0
+
+
 def setup_dist(args):
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world != args.gpus:
+        raise SystemExit(f"--gpus {args.gpus} but the launcher started WORLD_SIZE={world} ranks")
     ndev = torch.cuda.device_count()
-    if ndev and local >= ndev:  # rehearsal of N ranks on fewer GPUs (gloo); identity on a full node
+    # "nccl" is RCCL on ROCm; CZ_DIST_BACKEND=gloo rehearses N ranks on fewer GPUs (tests only)
+    backend = os.environ.get("CZ_DIST_BACKEND", "nccl") if world > 1 else None
+    if world > 1 and ndev < world and backend == "nccl":
+        raise SystemExit(f"{world} ranks need {world} GPUs for RCCL, {ndev} visible "
+                         "(CZ_DIST_BACKEND=gloo rehearses N ranks on one GPU)")
+    if ndev and local >= ndev:  # gloo rehearsal of N ranks on fewer GPUs; identity on a full node
         local %= ndev
     if world > 1:
         import torch.distributed as dist
         torch.cuda.set_device(local)
-        # "nccl" is RCCL on ROCm; CZ_DIST_BACKEND=gloo rehearses N ranks on one GPU
-        backend = os.environ.get("CZ_DIST_BACKEND", "nccl")
         if backend == "nccl":
             dist.init_process_group("nccl", device_id=torch.device(f"cuda:{local}"))
         else:
             dist.init_process_group(backend)
+        assert dist.get_world_size() == world
     else:
         torch.cuda.set_device(0)
     return world, rank, local
@@ -839,6 +894,8 @@ def roundtrip_leg(wl, world, steps):
 
 def main():
     args = parse()
+    if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
+        sys.exit(launch_ranks(args.gpus, sys.argv[1:]))
     world, rank, local = setup_dist(args)
     dev = torch.device(f"cuda:{local}")
     if args.config in ("e2e4k", "engine", "beforenm", "nacl"):
@@ -971,7 +1028,12 @@ def main():
         if sg is not None:
             line["scatter_gather"] = sg
         if per_rank is not None:
+            import torch.distributed as dist
+            assert len(per_rank) == world
             line["per_rank"] = per_rank
+            line["dist"] = {"backend": dist.get_backend(), "world_size": world,
+                            "gpus_visible": torch.cuda.device_count(),
+                            "rccl": dist.get_backend() == "nccl"}
         print(json.dumps(line), flush=True)
     if world > 1:
         import torch.distributed as dist

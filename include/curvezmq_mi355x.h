@@ -223,10 +223,12 @@ int cz_ctx_open(cz_ctx *ctx, const cz_frame_desc *h_desc, uint32_t count, const 
  * -> D2H on one of three streams with its own device buffers, so PCIe copies in both
  * directions overlap each other and the kernels.  A batch that is one chunk of at most
  * 64 MiB (in + out slots) of frames of 8+ blocks runs on one stream through the segment
- * kernels instead, so a few frames cost tens of us rather than one lane's whole walk; it
- * writes the bodies only and leaves slot padding as it was.  Rejected opens leave zeros in
- * their payload slots.  Host buffers should be pinned (cz_host_alloc) for full PCIe rate;
- * the output host buffer must span count * out_stride bytes (whole slots).  Uses the
+ * kernels instead, so a few frames cost tens of us rather than one lane's whole walk.  Both
+ * paths write whole output slots: each body followed by zeros to the end of its slot, and
+ * zeros in the payload slot of a rejected open, whatever the batch size or chunk_frames.
+ * For count == 1 the strides are ignored and the slot is the body alone.  Host buffers
+ * should be pinned (cz_host_alloc) for full PCIe rate; the output host buffer must span
+ * count * out_stride bytes (whole slots).  Uses the
  * context's key 0 (cz_ctx_set_keys).  Synchronous. */
 int cz_ctx_seal_uniform(cz_ctx *ctx, uint32_t count, uint32_t len, const void *h_in, uint64_t in_stride, void *h_out,
                         uint64_t out_stride, uint64_t counter0, const uint8_t *h_flags8, uint32_t chunk_frames);

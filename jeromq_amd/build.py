@@ -2,38 +2,144 @@
 
 The .so lands next to this file so it travels to the GPU box with the repo
 snapshot and is what jeromq_amd._lib loads.
+
+Every build is gated on the device ISA of the binary it produced (`isa_gate`): the gfx950 code
+objects are cut out of the linked library's .hip_fatbin, disassembled with llvm-objdump, and
+scanned by tools/isa_store_hazard.py for the VMEM store hazards the compiler does not count
+(store data rewritten at distance 1, a VALU-written SGPR read by VMEM within 5 states, a wide
+buffer store with a register soffset: DESIGN.md section 6).  A hit leaves the previous library in
+place and raises: a hazard in the shipped kernels writes wrong bytes silently.
 """
 import os
+import shutil
+import struct
 import subprocess
 import sys
+import tempfile
+from concurrent.futures import ThreadPoolExecutor
 
 HERE = os.path.dirname(os.path.abspath(__file__))
+ROOT = os.path.dirname(HERE)
 CSRC = os.path.join(HERE, "csrc")
 LIB = os.environ.get("CZ_LIB_OUT", os.path.join(HERE, "libcurvezmq_mi355x.so"))
 SOURCES = ["cz_kernels.hip", "cz_x25519.hip", "cz_host.cpp", "cz_mechanism.cpp", "cz_wire.cpp", "cz_engine.cpp", "cz_handshake.cpp", "cz_curve_hs.cpp"]
 HEADERS = ["cz_device.h", "cz_internal.h", "cz_salsa_lazy.h", os.path.join("..", "..", "include", "curvezmq_mi355x.h")]
 ARCH = os.environ.get("CZ_OFFLOAD_ARCH", "gfx950")
+LLVM_BIN = "/opt/rocm/lib/llvm/bin"
+BUNDLE_MAGIC = b"__CLANG_OFFLOAD_BUNDLE__"
 
 
-def _stale():
-    if not os.path.exists(LIB):
+class IsaHazardError(RuntimeError):
+    pass
+
+
+def _stale(lib=LIB, sources=SOURCES):
+    if not os.path.exists(lib):
         return True
-    t = os.path.getmtime(LIB)
-    return any(os.path.getmtime(os.path.join(CSRC, f)) > t for f in SOURCES + HEADERS)
+    t = os.path.getmtime(lib)
+    return any(os.path.getmtime(os.path.join(CSRC, f)) > t for f in list(sources) + HEADERS)
 
 
-def build_library(force=False, verbose=True):
-    if not force and not _stale():
-        return LIB
+def device_code_objects(so_path, arch=ARCH):
+    """The `arch` code objects (ELF) inside a HIP library's .hip_fatbin: one offload bundle per
+    translation unit, each `magic, u64 n, n x {u64 offset, u64 size, u64 triple_len, triple}`
+    with offsets from the bundle's start."""
+    with tempfile.TemporaryDirectory() as td:
+        fb = os.path.join(td, "fatbin")
+        subprocess.run([os.path.join(LLVM_BIN, "llvm-objcopy"), "--dump-section", f".hip_fatbin={fb}", so_path,
+                        os.path.join(td, "discard")], check=True, capture_output=True)
+        data = open(fb, "rb").read()
+    cos, i = [], data.find(BUNDLE_MAGIC)
+    while i >= 0:
+        (n,) = struct.unpack_from("<Q", data, i + len(BUNDLE_MAGIC))
+        p = i + len(BUNDLE_MAGIC) + 8
+        for _ in range(n):
+            off, size, tlen = struct.unpack_from("<QQQ", data, p)
+            triple = data[p + 24:p + 24 + tlen].decode()
+            p += 24 + tlen
+            if triple.endswith("--" + arch) and size:
+                cos.append(data[i + off:i + off + size])
+        i = data.find(BUNDLE_MAGIC, i + 1)
+    return cos
+
+
+def disassemble(code_object, arch=ARCH):
+    """llvm-objdump listing of one code object, reduced to instruction lines (no labels or
+    encoding comments), the form tools/isa_store_hazard.scan reads."""
+    with tempfile.NamedTemporaryFile(suffix=".co") as f:
+        f.write(code_object)
+        f.flush()
+        out = subprocess.run([os.path.join(LLVM_BIN, "llvm-objdump"), "-d", f"--mcpu={arch}", f.name],
+                             check=True, capture_output=True, text=True).stdout
+    lines = []
+    for ln in out.splitlines():
+        ln = ln.split("//")[0].rstrip()
+        if ln.strip() and not ln.endswith(":") and not ln.startswith(("Disassembly", "/")):
+            lines.append(ln)
+    return "\n".join(lines)
+
+
+def isa_gate(so_path, arch=ARCH):
+    """Scan every gfx950 code object of `so_path`; raise IsaHazardError on any hazard.
+    Returns (code objects, instructions scanned)."""
+    sys.path.insert(0, os.path.join(ROOT, "tools"))
+    from isa_store_hazard import scan
+    cos = device_code_objects(so_path, arch)
+    if not cos:
+        raise IsaHazardError(f"{so_path}: no {arch} code object found to scan")
+    total, hits = 0, []
+    for co in cos:
+        text = disassemble(co, arch)
+        total += text.count("\n") + 1
+        d, s, r = scan(text)
+        hits += [("store data rewritten at distance 1", x) for x in d]
+        hits += [("VALU-written SGPR read by VMEM within 5 states", x) for x in s]
+        hits += [("wide buffer store with a register soffset", x) for x in r]
+    if hits:
+        raise IsaHazardError(f"{so_path}: {len(hits)} VMEM store hazard(s) in the {arch} ISA, "
+                             f"library not installed; first: {hits[:3]}")
+    return len(cos), total
+
+
+def build_library(force=False, verbose=True, sources=None, lib=None, src_dir=None, jobs=None):
+    """Compile `sources` (default: the product sources in csrc/) in parallel, link `lib`, gate it on
+    the ISA scan, then move it into place."""
+    sources = list(sources or SOURCES)
+    lib = lib or LIB
+    src_dir = src_dir or CSRC
+    if not force and src_dir == CSRC and not _stale(lib, sources):
+        return lib
     hipcc = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
     extra = os.environ.get("CZ_EXTRA_FLAGS", "").split()  # A/B experiments only (e.g. -DCZ_SEAL_WAVES_PER_EU=5)
-    cmd = [hipcc, f"--offload-arch={ARCH}", "-O3", "-std=c++17", "-fPIC", "-shared", "-Wall",
-           "-o", LIB + ".tmp"] + extra + [os.path.join(CSRC, f) for f in SOURCES]
-    if verbose:
-        print(" ".join(cmd), file=sys.stderr)
-    subprocess.check_call(cmd, cwd=CSRC)
-    os.replace(LIB + ".tmp", LIB)
-    return LIB
+    common = [f"--offload-arch={arch}" for arch in [ARCH]] + ["-O3", "-std=c++17", "-fPIC", "-Wall"] + extra
+    objdir = tempfile.mkdtemp(prefix="cz_build_")
+    try:
+        def compile_one(f):
+            obj = os.path.join(objdir, os.path.splitext(f)[0] + ".o")
+            cmd = [hipcc] + common + ["-c", "-o", obj, os.path.join(src_dir, f)]
+            if verbose:
+                print(" ".join(cmd), file=sys.stderr)
+            r = subprocess.run(cmd, cwd=src_dir, capture_output=True, text=True)
+            if r.returncode:
+                raise subprocess.CalledProcessError(r.returncode, cmd, r.stdout, r.stderr)
+            return obj
+        # the largest translation unit first: the kernels dominate the build
+        order = sorted(sources, key=lambda f: -os.path.getsize(os.path.join(src_dir, f)))
+        with ThreadPoolExecutor(max_workers=jobs or min(len(order), os.cpu_count() or 4, 8)) as ex:
+            objs = list(ex.map(compile_one, order))
+        tmp = lib + ".tmp"
+        subprocess.check_call([hipcc, f"--offload-arch={ARCH}", "-shared", "-fPIC", "-o", tmp] + objs, cwd=src_dir)
+        try:
+            n_co, n_ins = isa_gate(tmp)
+        except Exception:
+            os.unlink(tmp)
+            raise
+        if verbose:
+            print(f"isa gate: {n_co} {ARCH} code objects, {n_ins} instructions, 0 store hazards", file=sys.stderr)
+        os.replace(tmp, lib)
+    finally:
+        shutil.rmtree(objdir, ignore_errors=True)
+    return lib
 
 
 if __name__ == "__main__":

@@ -191,6 +191,8 @@ static int nacl_one_launch(uint8_t *dst, const uint8_t *src, uint64_t len, const
     if ((e = czk_nacl_one(st, (uint32_t)len, open, (uint8_t *)s.subcache.ptr + 32 * slot, miss, (uint32_t)out_off, k, n,
                           s.stream)) != hipSuccess ||
         (e = hipStreamSynchronize(s.stream)) != hipSuccess) {
+        if (!open)
+            explicit_bzero(st + 128, len);  // the staged plaintext box (as Mechanism::seal_one)
         hip_fail(e, "cz_box (one launch)");
         return -1;
     }
@@ -198,6 +200,7 @@ static int nacl_one_launch(uint8_t *dst, const uint8_t *src, uint64_t len, const
         s.cvalid[slot] = true;
     const int rc = *(volatile int *)(st + 56);
     if (!open) {
+        explicit_bzero(st + 128, len);  // no plaintext left in the pinned staging after the call
         memset(dst, 0, 16);
         memcpy(dst + 16, st + out_off + 16, len - 16);
         return rc == 0 ? 0 : -1;
@@ -859,11 +862,6 @@ static int ctx_uniform_segments(cz_ctx *c, bool seal, uint32_t count, uint32_t l
                                 uint64_t in_stride, void *h_out, uint64_t out_stride, uint64_t counter0,
                                 const uint8_t *h_flags8, uint16_t *h_status, int check, uint32_t nblk)
 {
-    const uint64_t olen = seal ? (uint64_t)len + CZ_MESSAGE_OVERHEAD : (uint64_t)len - CZ_MESSAGE_OVERHEAD;
-    if (count == 1) {  // strides are not checked for one frame
-        in_stride = len;
-        out_stride = std::max<uint64_t>(olen, 1);
-    }
     const uint32_t seg = batch_seg_blocks((uint64_t)count * nblk, nblk);
     const uint32_t lead = seal ? 0u : 1u;
     const bool split = nblk > seg + seg / 2;
@@ -905,18 +903,19 @@ static int ctx_uniform_segments(cz_ctx *c, bool seal, uint32_t count, uint32_t l
     if ((e = hipMemcpyAsync(dm, hm, m_end, hipMemcpyHostToDevice, q)) != hipSuccess ||
         (e = hipMemcpyAsync(c->in.ptr, h_in, in_bytes, hipMemcpyHostToDevice, q)) != hipSuccess)
         return hip_fail(e, "H2D");
-    if (seal) {
-        e = czk_seal_segments(dd, ds, (uint32_t)nseg, dc, (uint32_t)ncomb, c->in.ptr, c->out.ptr, c->subkeys.ptr,
-                              c->work.ptr, q);
-    } else if ((e = hipMemsetAsync(c->out.ptr, 0, out_bytes, q)) == hipSuccess) {  // rejected frames: zeros
-        e = czk_open_segments(dd, ds, (uint32_t)nseg, dc, (uint32_t)ncomb, c->in.ptr, c->out.ptr, c->subkeys.ptr,
-                              c->work.ptr, (uint16_t *)c->status.ptr, nullptr, q);
+    // whole slots, as the pipelined path returns them: the body, then zeros to the slot's end (and
+    // zeros in a rejected open's slot)
+    if ((e = hipMemsetAsync(c->out.ptr, 0, out_bytes, q)) == hipSuccess) {
+        if (seal)
+            e = czk_seal_segments(dd, ds, (uint32_t)nseg, dc, (uint32_t)ncomb, c->in.ptr, c->out.ptr, c->subkeys.ptr,
+                                  c->work.ptr, q);
+        else
+            e = czk_open_segments(dd, ds, (uint32_t)nseg, dc, (uint32_t)ncomb, c->in.ptr, c->out.ptr, c->subkeys.ptr,
+                                  c->work.ptr, (uint16_t *)c->status.ptr, nullptr, q);
     }
     if (e != hipSuccess)
         return hip_fail(e, "launch");
-    // the bodies only: the caller's slot padding is left as it was
-    if ((olen && (e = hipMemcpy2DAsync(h_out, out_stride, c->out.ptr, out_stride, olen, count, hipMemcpyDeviceToHost,
-                                       q)) != hipSuccess) ||
+    if ((e = hipMemcpyAsync(h_out, c->out.ptr, out_bytes, hipMemcpyDeviceToHost, q)) != hipSuccess ||
         (!seal && (e = hipMemcpyAsync(h_status, c->status.ptr, 2ull * count, hipMemcpyDeviceToHost, q)) != hipSuccess) ||
         (e = hipStreamSynchronize(q)) != hipSuccess)
         return hip_fail(e, "D2H");
@@ -945,6 +944,10 @@ static int ctx_uniform(cz_ctx *c, bool seal, uint32_t count, uint32_t len, const
         return fail(CZ_EINVAL, "cz_ctx_*_uniform: stride smaller than a frame");
     if (count == 0)
         return CZ_OK;
+    if (count == 1) {  // strides are not checked for one frame: its slot is the frame itself
+        in_stride = len;
+        out_stride = std::max<uint64_t>(olen, 1);
+    }
     // a single-chunk batch of multi-block frames: the segment kernels (one stream)
     const uint64_t nblk = ((seal ? (uint64_t)len + CZ_MESSAGE_OVERHEAD : (uint64_t)len) + 63) / 64;
     static const bool lanes_only = getenv("CZ_CTX_LANES_ONLY") != nullptr;  // A/B: the lane-per-frame kernel
@@ -1000,8 +1003,12 @@ static int ctx_uniform(cz_ctx *c, bool seal, uint32_t count, uint32_t len, const
                             (reuse && (e = hipStreamWaitEvent(s_k, c->ev_out[q], 0)) != hipSuccess)))
             return hip_fail(e, "event");
         if (seal) {
-            e = czk_seal_uniform(c->pin[q].ptr, in_stride, c->pout[q].ptr, out_stride, nc, len, c->subkeys.ptr,
-                                 counter0 + f0, dfl, s_k);
+            // a slot stride off the 128-byte lines leaves the bytes between bodies to the caller
+            // (cz_seal_uniform): zero them, so the host gets whole slots on every path
+            e = out_stride % 128 ? hipMemsetAsync(c->pout[q].ptr, 0, (uint64_t)nc * out_stride, s_k) : hipSuccess;
+            if (e == hipSuccess)
+                e = czk_seal_uniform(c->pin[q].ptr, in_stride, c->pout[q].ptr, out_stride, nc, len, c->subkeys.ptr,
+                                     counter0 + f0, dfl, s_k);
         } else {
             // the chunk's first frame must beat the previous chunk's last nonce: read it from the host copy
             uint64_t floor0 = counter0;

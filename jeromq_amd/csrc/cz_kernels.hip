@@ -626,7 +626,8 @@ __device__ __forceinline__ void seal_frame(const uint8_t *__restrict__ in0, u32 
     const u32 mlen = (MODE == MODE_ZMQ || MODE == MODE_BOX) ? n + 33u : n;
     const u32 nfull = mlen >> 6;
     const u32 tailv = mlen & 63u;
-    const u64 inlen = MODE == MODE_BOX ? (u64)mlen : (u64)n - ina_d;  // bytes from `in`
+    // bytes from `in`; a payload shorter than d lies wholly in P[-1] (pm1)
+    const u64 inlen = MODE == MODE_BOX ? (u64)mlen : (n > ina_d ? (u64)(n - ina_d) : 0ull);
     u32 n0, n1;
     counter_nonce(counter, n0, n1);
     if constexpr (UN0)
@@ -1785,7 +1786,10 @@ __device__ __forceinline__ void seal_segment(const uint8_t *__restrict__ in0, u3
     const u32 nfull = mlen >> 6;
     const u32 bend = b1 < nblk ? b1 : nblk;
     const u32 nch = bend - b0;
-    const u64 inlen = (u64)n - ina_d;  // bytes from `in`
+    // bytes from `in`.  A payload of 0..2 bytes at an odd offset is shorter than d = -in0 & 3 and
+    // lies wholly in P[-1] (pm1): no load may read past it (n - d would wrap to ~2^64, and the pair
+    // loop would then read up to 128 bytes past the payload).
+    const u64 inlen = n > ina_d ? (u64)(n - ina_d) : 0ull;
     u32 n0, n1;
     counter_nonce(counter, n0, n1);
     u32 x[16], C[16];

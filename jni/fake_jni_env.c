@@ -1,0 +1,175 @@
+/* fake_jni_env.c -- test double of a JVM's JNIEnv for tests/test_jni_shim.py (test infrastructure,
+ * never shipped).  Builds the JNINativeInterface_ table of jni_min.h with the slots the shim calls
+ * and fake Java objects behind jobject: byte[] / int[] arrays over host buffers the test owns,
+ * direct ByteBuffers, ByteBuffer[] and a class handle.  Records every pin and release (and its
+ * mode) so the test can check the shim's JNI discipline, and can emulate a VM that hands out COPIES
+ * from GetPrimitiveArrayCritical (released with mode 0 = copy back, JNI_ABORT = discard), so a
+ * wrong release mode shows up as wrong bytes in the Java array. */
+#include <stdlib.h>
+#include <string.h>
+
+#include "jni_min.h"
+
+enum { K_BYTES = 1, K_INTS, K_DIRECT, K_CLASS, K_OBJARRAY };
+
+struct _jobject {
+    int kind;
+    jsize len;      /* array elements */
+    void *data;     /* array storage (owned by the test) or direct buffer address (NULL: not direct) */
+    jlong cap;      /* direct buffer capacity */
+    int pins, releases, last_mode;
+    void *copy;     /* the live copy handed out in copy mode */
+    jobject *elems; /* K_OBJARRAY */
+};
+
+static int g_copy_mode, g_fail_pin_at = -1, g_pin_count, g_outstanding, g_calls_in_critical;
+static int g_modes[64], g_nmodes;
+
+static size_t elem_size(jobject o) { return o->kind == K_INTS ? 4 : 1; }
+
+static jclass f_FindClass(JNIEnv *env, const char *name)
+{
+    (void)env;
+    static struct _jobject cls = {K_CLASS, 0, NULL, 0, 0, 0, 0, NULL, NULL};
+    if (g_outstanding)
+        g_calls_in_critical++;
+    return strcmp(name, "java/nio/ByteBuffer") == 0 ? &cls : NULL;
+}
+
+static jsize f_GetArrayLength(JNIEnv *env, jarray a)
+{
+    (void)env;
+    if (g_outstanding)
+        g_calls_in_critical++;
+    return a->len;
+}
+
+static jobjectArray f_NewObjectArray(JNIEnv *env, jsize len, jclass cls, jobject init)
+{
+    (void)env, (void)cls, (void)init;
+    jobject o = (jobject)calloc(1, sizeof *o);
+    o->kind = K_OBJARRAY;
+    o->len = len;
+    o->elems = (jobject *)calloc(len ? (size_t)len : 1, sizeof(jobject));
+    return o;
+}
+
+static void f_SetObjectArrayElement(JNIEnv *env, jobjectArray a, jsize i, jobject v)
+{
+    (void)env;
+    if (i >= 0 && i < a->len)
+        a->elems[i] = v;
+}
+
+static void f_SetIntArrayRegion(JNIEnv *env, jintArray a, jsize start, jsize len, const jint *buf)
+{
+    (void)env;
+    if (start >= 0 && start + len <= a->len)
+        memcpy((jint *)a->data + start, buf, (size_t)len * 4);
+}
+
+static void *f_GetPrimitiveArrayCritical(JNIEnv *env, jarray a, jboolean *isCopy)
+{
+    (void)env;
+    if (g_pin_count++ == g_fail_pin_at)
+        return NULL;
+    a->pins++;
+    g_outstanding++;
+    if (isCopy)
+        *isCopy = (jboolean)g_copy_mode;
+    if (!g_copy_mode)
+        return a->data;
+    const size_t n = (size_t)a->len * elem_size(a);
+    a->copy = malloc(n ? n : 1);
+    memcpy(a->copy, a->data, n);
+    return a->copy;
+}
+
+static void f_ReleasePrimitiveArrayCritical(JNIEnv *env, jarray a, void *p, jint mode)
+{
+    (void)env;
+    a->releases++;
+    a->last_mode = mode;
+    g_outstanding--;
+    if (g_nmodes < 64)
+        g_modes[g_nmodes++] = mode;
+    if (g_copy_mode && p == a->copy) {
+        if (mode != JNI_ABORT)
+            memcpy(a->data, p, (size_t)a->len * elem_size(a));
+        if (mode != JNI_COMMIT) {
+            free(a->copy);
+            a->copy = NULL;
+        }
+    }
+}
+
+static jobject f_NewDirectByteBuffer(JNIEnv *env, void *p, jlong cap)
+{
+    (void)env;
+    jobject o = (jobject)calloc(1, sizeof *o);
+    o->kind = K_DIRECT;
+    o->data = p;
+    o->cap = cap;
+    return o;
+}
+
+static void *f_GetDirectBufferAddress(JNIEnv *env, jobject b)
+{
+    (void)env;
+    return b && b->kind == K_DIRECT ? b->data : NULL;
+}
+
+static jlong f_GetDirectBufferCapacity(JNIEnv *env, jobject b)
+{
+    (void)env;
+    return b && b->kind == K_DIRECT && b->data ? b->cap : -1;
+}
+
+static struct JNINativeInterface_ g_table;
+static const struct JNINativeInterface_ *g_env = &g_table;
+
+JNIEnv *fake_env(void)
+{
+    g_table.FindClass = f_FindClass;
+    g_table.GetArrayLength = f_GetArrayLength;
+    g_table.NewObjectArray = f_NewObjectArray;
+    g_table.SetObjectArrayElement = f_SetObjectArrayElement;
+    g_table.SetIntArrayRegion = f_SetIntArrayRegion;
+    g_table.GetPrimitiveArrayCritical = f_GetPrimitiveArrayCritical;
+    g_table.ReleasePrimitiveArrayCritical = f_ReleasePrimitiveArrayCritical;
+    g_table.NewDirectByteBuffer = f_NewDirectByteBuffer;
+    g_table.GetDirectBufferAddress = f_GetDirectBufferAddress;
+    g_table.GetDirectBufferCapacity = f_GetDirectBufferCapacity;
+    return (JNIEnv *)&g_env;
+}
+
+static jobject new_obj(int kind, void *data, jsize len, jlong cap)
+{
+    jobject o = (jobject)calloc(1, sizeof *o);
+    o->kind = kind;
+    o->data = data;
+    o->len = len;
+    o->cap = cap;
+    return o;
+}
+
+jobject fake_byte_array(void *data, jsize len) { return new_obj(K_BYTES, data, len, 0); }
+jobject fake_int_array(void *data, jsize len) { return new_obj(K_INTS, data, len, 0); }
+jobject fake_direct(void *p, jlong cap) { return new_obj(K_DIRECT, p, 0, cap); }
+jobject fake_heap_buffer(void) { return new_obj(K_DIRECT, NULL, 0, 0); } /* a non-direct ByteBuffer */
+
+void fake_set_copy_mode(int on) { g_copy_mode = on; }
+void fake_fail_pin_at(int n) { g_fail_pin_at = n, g_pin_count = 0; }
+void fake_reset_log(void) { g_nmodes = 0, g_calls_in_critical = 0, g_pin_count = 0, g_fail_pin_at = -1; }
+int fake_outstanding(void) { return g_outstanding; }
+int fake_calls_in_critical(void) { return g_calls_in_critical; }
+int fake_nmodes(void) { return g_nmodes; }
+int fake_mode(int i) { return i >= 0 && i < g_nmodes ? g_modes[i] : -1; }
+int fake_pins(jobject o) { return o->pins; }
+int fake_releases(jobject o) { return o->releases; }
+int fake_last_mode(jobject o) { return o->last_mode; }
+int fake_kind(jobject o) { return o ? o->kind : 0; }
+jsize fake_len(jobject o) { return o->len; }
+jobject fake_elem(jobject o, jsize i) { return o->elems[i]; }
+void *fake_addr(jobject o) { return o->data; }
+jlong fake_cap(jobject o) { return o->cap; }

@@ -176,3 +176,69 @@ def test_frame_range_and_byte_balance():
     work = [int((lens[b[r]:b[r + 1]] + 33).sum()) for r in range(8)]
     assert max(work) - min(work) <= 2 * (64 * 1024 + 33)   # within ~one max frame of each other
     assert shard.balance_by_bytes([], 4) == [0, 0, 0, 0, 0]
+
+
+class _FakePopen:
+    """Stands in for the child torch.distributed.run: records the command, replays canned stdout."""
+
+    def __init__(self, out, rc=0):
+        self.out, self.rc, self.cmd = out, rc, None
+
+    def __call__(self, cmd, **kw):
+        self.cmd, self.kw = cmd, kw
+        self.stdout = iter(self.out)
+        return self
+
+    def wait(self):
+        return self.rc
+
+
+def _rank_line(n):
+    import json
+    return json.dumps({"metric": "m", "value": 1.0, "n_gpus": n,
+                       "per_rank": [{"rank": r, "kernel_ms": 2.0} for r in range(n)]}) + "\n"
+
+
+def test_bench_gpus_n_launches_child_ranks_without_touching_gpu(capsys):
+    """`python bench.py --gpus N` (no launcher): bench starts torch.distributed.run with N ranks as a
+    child process, never initialises the GPU itself, and relays exactly one checked JSON line."""
+    import json
+    import bench
+    fake = _FakePopen(["rank chatter\n", _rank_line(8)])
+    rc = bench.launch_ranks(8, ["--gpus", "8", "--steps", "5"], popen=fake)
+    assert rc == 0
+    assert fake.cmd[1:4] == ["-m", "torch.distributed.run", "--nnodes=1"]
+    assert "--nproc-per-node=8" in fake.cmd and "127.0.0.1" in fake.cmd
+    assert fake.cmd[-4:] == ["--gpus", "8", "--steps", "5"]
+    assert fake.kw["env"]["HSA_ENABLE_IPC_MODE_LEGACY"] == "0"
+    assert not torch.cuda.is_initialized()
+    out = capsys.readouterr()
+    lines = [ln for ln in out.out.splitlines() if ln.startswith("{")]
+    assert len(lines) == 1 and json.loads(lines[0])["n_gpus"] == 8
+    assert "rank chatter" in out.err
+
+
+@pytest.mark.parametrize("out,rc", [
+    ([_rank_line(1)], 0),                    # ranks timed fewer GPUs than asked
+    ([_rank_line(2), _rank_line(2)], 0),     # more than one JSON line
+    ([], 0),                                 # no line at all
+    ([_rank_line(2)], 3),                    # a rank failed: its exit status is passed on
+])
+def test_bench_launcher_rejects_bad_rank_output(out, rc, capsys):
+    import bench
+    got = bench.launch_ranks(2, ["--gpus", "2"], popen=_FakePopen(out, rc))
+    assert got == (rc if rc else 1)
+    assert not [ln for ln in capsys.readouterr().out.splitlines() if ln.startswith("{")]
+
+
+def test_bench_refuses_world_size_mismatch(monkeypatch):
+    """Under a launcher, WORLD_SIZE must equal --gpus (a mismatch would mislabel the scaling line)."""
+    import argparse
+    import bench
+    monkeypatch.setenv("WORLD_SIZE", "4")
+    with pytest.raises(SystemExit, match="WORLD_SIZE=4"):
+        bench.setup_dist(argparse.Namespace(gpus=8))
+    monkeypatch.setenv("WORLD_SIZE", "2")
+    monkeypatch.delenv("CZ_DIST_BACKEND", raising=False)
+    with pytest.raises(SystemExit, match="need 2 GPUs for RCCL"):   # no GPU here: nccl refused, not faked
+        bench.setup_dist(argparse.Namespace(gpus=2))

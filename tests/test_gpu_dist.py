@@ -111,3 +111,26 @@ def test_bench_ws2_rehearsal():
     assert line["scatter_gather"]["verified"] and line["seal_open_verify"]["verified"]
     assert [p["rank"] for p in line["per_rank"]] == [0, 1]
     assert all(p["hbm_frac"] > 0 for p in line["per_rank"])
+
+
+def test_bench_plain_gpus2_launches_its_own_ranks():
+    """`python bench.py --gpus 2` with no launcher (how the driver runs N=1): bench.py starts the two
+    ranks itself as a child torch.distributed.run and the line covers both (gloo on one GPU here;
+    RCCL on the driver's 8-GPU node)."""
+    import torch
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    env = dict(os.environ, CZ_DIST_BACKEND="gloo", TMPDIR="/tmp")
+    for k in ("WORLD_SIZE", "RANK", "LOCAL_RANK", "MASTER_ADDR", "MASTER_PORT"):
+        env.pop(k, None)
+    cmd = [sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "2", "--steps", "3", "--warmup", "1",
+           "--ramp-ms", "0", "--frames", "65536"]
+    r = subprocess.run(cmd, capture_output=True, text=True, timeout=300, env=env, cwd=ROOT)
+    assert r.returncode == 0, r.stderr[-3000:]
+    lines = [ln for ln in r.stdout.splitlines() if ln.startswith("{")]
+    assert len(lines) == 1, r.stdout[-2000:]
+    line = json.loads(lines[0])
+    assert line["n_gpus"] == 2 and len(line["per_rank"]) == 2
+    assert line["dist"]["world_size"] == 2 and line["dist"]["backend"] == "gloo"
+    assert line["scatter_gather"]["verified"] and line["seal_open_verify"]["verified"]
+    assert line["launcher"].startswith("bench.py --gpus")

@@ -676,8 +676,8 @@ def test_ctx_uniform_default_chunks(L, torch_dev):
                                              (7, 20000, 20000, 20040)])
 def test_ctx_uniform_small_segmented(L, torch_dev, count, n, ist, ost):
     """Small host-staged uniform batches of multi-block frames (one chunk, <= 4 MiB) run the
-    segment kernels, segment-major: every body against the oracle, the caller's slot padding left
-    alone, the open round trip, and rejected frames (bad tag, replay, wrong command) with zeros in
+    segment kernels, segment-major: every body against the oracle, zeros in the slot padding
+    (whole slots, as the pipelined path writes them), the open round trip, and rejected frames (bad tag, replay, wrong command) with zeros in
     their payload slots."""
     lib = L.lib()
     ctx = ctypes.c_void_p()
@@ -693,7 +693,7 @@ def test_ctx_uniform_small_segmented(L, torch_dev, count, n, ist, ost):
         for i in range(count):
             body = hout[i * so:i * so + n + 33].tobytes()
             assert body == or_curve_encode(hin[i * si:i * si + n].tobytes(), int(flags[i]), 11 + i, 0, PRECOM), i
-            assert np.all(hout[i * so + n + 33:(i + 1) * so] == 0xCD), i
+            assert not hout[i * so + n + 33:(i + 1) * so].any(), i
         back = np.full(count * si, 0xEE, dtype=np.uint8)
         st = np.full(count, 0xFFFF, dtype=np.uint16)
         L.check(lib.cz_ctx_open_uniform(ctx, count, n + 33, hout.ctypes.data, ost, back.ctypes.data, ist, 10, 1,
@@ -718,6 +718,45 @@ def test_ctx_uniform_small_segmented(L, torch_dev, count, n, ist, ost):
             assert not back[i * si:i * si + n].any(), i
         for i in (4, 18, 41, count - 1):
             assert np.array_equal(back[i * si:i * si + n], hin[i * si:i * si + n]), i
+    finally:
+        lib.cz_ctx_destroy(ctx)
+
+
+@pytest.mark.parametrize("n,ist,ost", [(4096, 4096, 4224), (1000, 1003, 1100)])
+def test_ctx_uniform_paths_write_identical_whole_slots(L, torch_dev, n, ist, ost):
+    """the one-chunk segment path (chunk_frames 0) and the pipelined path (chunks of 64
+    frames) return byte-identical output buffers for the same frames -- bodies, zero slot padding,
+    and for the open zeros in a rejected frame's slot -- into host buffers pre-filled with garbage."""
+    lib = L.lib()
+    ctx = ctypes.c_void_p()
+    L.check(lib.cz_ctx_create(ctypes.byref(ctx), 0))
+    try:
+        L.check(lib.cz_ctx_set_keys(ctx, PRECOM, 1, L.CZ_DIR_C2S))
+        count = 300
+        hin = np.frombuffer(splitmix_bytes(count * ist, 5 + n), dtype=np.uint8).copy()
+        outs, backs = [], []
+        for chunk, fill in ((0, 0xCD), (64, 0x5A)):
+            hout = np.full(count * ost, fill, dtype=np.uint8)
+            L.check(lib.cz_ctx_seal_uniform(ctx, count, n, hin.ctypes.data, ist, hout.ctypes.data, ost, 9, None,
+                                            chunk))
+            outs.append(hout)
+        assert np.array_equal(outs[0], outs[1])
+        slots = outs[0].reshape(count, ost)
+        assert not slots[:, n + 33:].any()
+        assert slots[7, :n + 33].tobytes() == or_curve_encode(hin[7 * ist:7 * ist + n].tobytes(), 0, 16, 0, PRECOM)
+        bad = outs[0].copy()
+        bad[3 * ost + 60] ^= 1
+        for chunk, fill in ((0, 0xEE), (64, 0x11)):
+            back = np.full(count * ist, fill, dtype=np.uint8)
+            st = np.zeros(count, dtype=np.uint16)
+            L.check(lib.cz_ctx_open_uniform(ctx, count, n + 33, bad.ctypes.data, ost, back.ctypes.data, ist, 8, 1,
+                                            st.ctypes.data, chunk))
+            assert (st[3] & 0xff) == L.CZ_STATUS_CRYPTO and np.count_nonzero(st & 0xff) == 1
+            backs.append(back)
+        assert np.array_equal(backs[0], backs[1])
+        plain = backs[0].reshape(count, ist)
+        assert not plain[3].any() and not plain[:, n:].any()
+        assert np.array_equal(plain[4, :n], hin[4 * ist:4 * ist + n])
     finally:
         lib.cz_ctx_destroy(ctx)
 

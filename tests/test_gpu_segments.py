@@ -373,3 +373,32 @@ def test_zipf_seal_payloads_at_any_offset(torch_dev, subkeys, L, in_round, out_r
             assert bad.size == 0, f"seal_ina={v}: {bad.size} bytes differ, first at {int(bad[0])}"
     finally:
         lib.cz_tune(b"seal_ina", old)
+
+
+@pytest.mark.parametrize("seal_ina", [1, 0])
+def test_seal_segments_tiny_payloads_at_odd_offsets_end_of_buffer(torch_dev, subkeys, L, seal_ina):
+    """0..2-byte payloads at byte offsets 1..3 mod 4 are shorter than the distance d to
+    their first dword boundary; the any-offset segment seal must read nothing past them (its byte
+    count from the dword boundary is clamped to 0, the payload lives in P[-1]).  Full waves of such
+    frames, packed back to back, the last payload ending exactly at the end of the input buffer and
+    the last body at the end of the output buffer; every body against the oracle."""
+    torch, dev = torch_dev
+    rng = np.random.default_rng(5)
+    lens = [int(x) for x in rng.choice([0, 1, 2, 0, 1, 2, 3, 5], size=256)]
+    desc = np.zeros(len(lens), dtype=DESC_DTYPE)
+    io, oo = 1, 3          # odd starts: every payload at some byte offset mod 4
+    for i, n in enumerate(lens):
+        desc[i] = (io, oo, n, 0, 7 + 3 * i, i & 3, -1)
+        io += n
+        oo += n + 33
+    assert (desc["in_off"] % 4 != 0).sum() > len(lens) // 2
+    hin = np.frombuffer(splitmix_bytes(io, 99), dtype=np.uint8).copy()   # no slack past the last payload
+    want = _oracle_seal(desc, hin, oo)
+    lib = L.lib()
+    old = lib.cz_tune(b"seal_ina", seal_ina)
+    try:
+        out, plan = _seal_seg(torch_dev, subkeys, desc, hin, oo, 64)
+    finally:
+        lib.cz_tune(b"seal_ina", old)
+    bad = np.nonzero(out != want)[0]
+    assert bad.size == 0, f"{bad.size} bytes differ, first at {int(bad[0])}"

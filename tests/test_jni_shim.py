@@ -1,0 +1,317 @@
+"""The JNI binding (jni/curvezmq_jni.c, INTEGRATION.md sections 2-3) compiled and driven through a
+fake JNIEnv (jni/fake_jni_env.c) -- there is no JDK in this image, so jni/jni_min.h restates the JNI
+types and the function-table slots the shim calls (indices pinned by static asserts).
+
+CPU: the shim compiles with -Wall -Wextra -Werror; every Java native the INTEGRATION classes declare
+is exported under its JNI-mangled name; short / null arrays and wrong direct buffers are refused
+before anything is pinned or the library entered; a failed pin releases what was pinned; inputs are
+released with JNI_ABORT and outputs with 0; no JNI call happens inside a critical region.
+GPU: one MESSAGE box sealed and opened through the jnacl natives (in a VM that hands out copies),
+a uniform batch through GpuCurveBatch over direct buffers, and an engine round trip through
+GpuCurveEngine, all against the oracle."""
+import ctypes
+import os
+import subprocess
+
+import numpy as np
+import pytest
+
+from cz_testlib import or_curve_encode, splitmix_bytes, v2_encode
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+JNI = os.path.join(ROOT, "jni")
+LIBDIR = os.path.join(ROOT, "jeromq_amd")
+PRECOM = bytes.fromhex("0e8790cb0dc8703af2533cc8594eecfbf62ca560a66ebee1259cc0a30435c6f3")
+JNI_ABORT = 2
+CZ_EINVAL = -22
+
+JNACL = "Java_com_neilalexander_jnacl_crypto_curve25519xsalsa20poly1305_"
+SECRETBOX = "Java_com_neilalexander_jnacl_crypto_xsalsa20poly1305_"
+BATCH = "Java_zmq_io_mechanism_curve_GpuCurveBatch_"
+ENGINE = "Java_zmq_io_GpuCurveEngine_"
+# the natives the Java classes of INTEGRATION.md declare, JNI-mangled ('_' in a name -> '_1')
+NATIVES = ([JNACL + n for n in ("crypto_1box_1afternm", "crypto_1box_1open_1afternm", "crypto_1box_1beforenm",
+                                "crypto_1box", "crypto_1box_1open", "crypto_1box_1keypair")]
+           + [SECRETBOX + n for n in ("crypto_1secretbox", "crypto_1secretbox_1open")]
+           + [BATCH + n for n in ("create", "destroy", "setKeys", "seal", "open", "sealUniform", "openUniform",
+                                  "hostAlloc", "hostFree")]
+           + [ENGINE + n for n in ("create", "destroy", "addConn", "msgAlloc", "send", "flushOut", "wireOut",
+                                   "wireIov", "recv", "flushIn", "msgsIn", "msgIn", "connError")])
+
+vp, i32, i64 = ctypes.c_void_p, ctypes.c_int32, ctypes.c_int64
+
+
+@pytest.fixture(scope="module")
+def shim(tmp_path_factory):
+    if not os.path.exists(os.path.join(LIBDIR, "libcurvezmq_mi355x.so")):
+        pytest.skip("library not built")
+    out = str(tmp_path_factory.mktemp("jni") / "libcz_jni_test.so")
+    subprocess.run(["gcc", "-std=c11", "-O2", "-Wall", "-Wextra", "-Werror", "-DCZ_JNI_MIN", "-shared", "-fPIC",
+                    "-I" + JNI, "-I" + os.path.join(ROOT, "include"), os.path.join(JNI, "curvezmq_jni.c"),
+                    os.path.join(JNI, "fake_jni_env.c"), "-L" + LIBDIR, "-lcurvezmq_mi355x",
+                    "-Wl,-rpath," + LIBDIR, "-o", out], check=True)
+    L = ctypes.CDLL(out)
+    for f in ("fake_env", "fake_byte_array", "fake_int_array", "fake_direct", "fake_heap_buffer", "fake_elem",
+              "fake_addr"):
+        getattr(L, f).restype = vp
+    L.fake_byte_array.argtypes = [vp, i32]
+    L.fake_int_array.argtypes = [vp, i32]
+    L.fake_direct.argtypes = [vp, i64]
+    L.fake_cap.restype = i64
+    for f in ("fake_pins", "fake_releases", "fake_last_mode", "fake_kind", "fake_len", "fake_addr", "fake_cap"):
+        getattr(L, f).argtypes = [vp]
+    L.fake_elem.argtypes = [vp, i32]
+    for n in NATIVES:
+        fn = getattr(L, n)
+        fn.restype = vp if n.endswith(("hostAlloc", "msgAlloc", "wireOut", "wireIov", "msgIn")) else i32
+        if n.startswith((JNACL, SECRETBOX)):   # (env, cls, byte[] ..., int len, byte[] ...)
+            fn.argtypes = ([vp, vp, vp, vp, i32, vp, vp] if "afternm" in n or "secretbox" in n
+                           else [vp, vp, vp, vp, i32, vp, vp, vp] if n.endswith(("crypto_1box", "crypto_1box_1open"))
+                           else [vp, vp, vp, vp, vp] if n.endswith("beforenm") else [vp, vp, vp, vp])
+    getattr(L, BATCH + "create").restype = i64
+    getattr(L, ENGINE + "create").restype = i64
+    L.env = L.fake_env()
+    return L
+
+
+class Arr:
+    """A Java byte[] / int[] over a numpy buffer."""
+
+    def __init__(self, L, data, ints=False):
+        self.np = np.ascontiguousarray(data)
+        self.obj = (L.fake_int_array if ints else L.fake_byte_array)(self.np.ctypes.data, len(self.np))
+        self.L = L
+
+    def pins(self):
+        return self.L.fake_pins(self.obj)
+
+    def releases(self):
+        return self.L.fake_releases(self.obj)
+
+    def mode(self):
+        return self.L.fake_last_mode(self.obj)
+
+
+def _u8(b):
+    return np.frombuffer(bytes(b), dtype=np.uint8).copy()
+
+
+def _box_args(L, mlen=132, n_len=24, k_len=32, c_len=None):
+    m = np.zeros(mlen, dtype=np.uint8)
+    m[32:] = _u8(splitmix_bytes(mlen - 32, 3))
+    return (Arr(L, np.zeros(c_len if c_len is not None else mlen, dtype=np.uint8)), Arr(L, m),
+            Arr(L, _u8(b"CurveZMQMESSAGEC" + (3).to_bytes(8, "big"))[:n_len]), Arr(L, _u8(PRECOM)[:k_len]))
+
+
+def test_shim_compiles_and_exports_every_native(shim):
+    nm = subprocess.run(["nm", "-D", "--defined-only", shim._name], capture_output=True, text=True, check=True).stdout
+    syms = {ln.split()[-1] for ln in nm.splitlines() if ln.strip()}
+    missing = [n for n in NATIVES if n not in syms]
+    assert not missing, missing
+    # the committed Java declarations (jni/java) mangle to exactly these natives
+    import re
+    declared = set()
+    for dp, _, files in os.walk(os.path.join(JNI, "java")):
+        for f in files:
+            src = open(os.path.join(dp, f)).read()
+            pkg = re.search(r"^package ([\w.]+);", src, re.M).group(1)
+            cls = f[:-len(".java")]
+            for meth in re.findall(r"static native [\w\[\]]+ (\w+)\(", src):
+                declared.add("Java_" + (pkg + "." + cls).replace("_", "_1").replace(".", "_") + "_"
+                             + meth.replace("_", "_1"))
+    assert declared == set(NATIVES), declared ^ set(NATIVES)
+
+
+@pytest.mark.parametrize("case", ["short_c", "short_m", "short_nonce", "short_key", "mlen_below_32", "null_m"])
+def test_jnacl_length_guards_pin_nothing(shim, case):
+    L = shim
+    L.fake_reset_log()
+    mlen = 132
+    kw = {"short_c": dict(c_len=131), "short_nonce": dict(n_len=23), "short_key": dict(k_len=31)}.get(case, {})
+    c, m, n, k = _box_args(L, mlen=mlen, **kw)
+    marg = None if case == "null_m" else m.obj
+    if case == "short_m":
+        m = Arr(L, np.zeros(mlen - 1, dtype=np.uint8))
+        marg = m.obj
+    if case == "mlen_below_32":
+        mlen = 31
+    rc = getattr(L, JNACL + "crypto_1box_1afternm")(L.env, None, c.obj, marg, mlen, n.obj, k.obj)
+    assert rc == -1
+    assert L.fake_nmodes() == 0 and L.fake_outstanding() == 0
+    assert all(a.pins() == 0 for a in (c, m, n, k))
+
+
+def test_jnacl_failed_pin_releases_what_it_pinned(shim):
+    L = shim
+    c, m, n, k = _box_args(L)
+    L.fake_reset_log()
+    L.fake_fail_pin_at(2)          # the nonce's pin fails after c and m were pinned
+    rc = getattr(L, JNACL + "crypto_1box_1afternm")(L.env, None, c.obj, m.obj, 132, n.obj, k.obj)
+    L.fake_reset_log()
+    assert rc == -1 and L.fake_outstanding() == 0
+    assert c.releases() == 1 and m.releases() == 1 and n.pins() == 0 and k.pins() == 0
+    assert c.mode() == JNI_ABORT and m.mode() == JNI_ABORT   # nothing was written: nothing copied back
+
+
+def test_jnacl_release_modes_and_no_jni_in_critical(shim):
+    """A full call (on a machine without a GPU the library returns -1; on a GPU it seals): the output
+    array is released with 0, every input with JNI_ABORT, each exactly once, in reverse order, and no
+    JNI function is called while the arrays are pinned."""
+    L = shim
+    for fn, outs in ((JNACL + "crypto_1box_1afternm", 1), (JNACL + "crypto_1box_1open_1afternm", 1),
+                     (SECRETBOX + "crypto_1secretbox", 1), (SECRETBOX + "crypto_1secretbox_1open", 1)):
+        c, m, n, k = _box_args(L)
+        L.fake_reset_log()
+        getattr(L, fn)(L.env, None, c.obj, m.obj, 132, n.obj, k.obj)
+        assert L.fake_outstanding() == 0 and L.fake_calls_in_critical() == 0
+        assert [a.pins() for a in (c, m, n, k)] == [1, 1, 1, 1]
+        assert [a.releases() for a in (c, m, n, k)] == [1, 1, 1, 1]
+        assert c.mode() == 0 and m.mode() == JNI_ABORT and n.mode() == JNI_ABORT and k.mode() == JNI_ABORT
+        assert [L.fake_mode(i) for i in range(4)] == [JNI_ABORT, JNI_ABORT, JNI_ABORT, 0]   # k, n, m, then c
+    pk, sk = Arr(L, np.zeros(32, np.uint8)), Arr(L, np.zeros(32, np.uint8))
+    L.fake_reset_log()
+    getattr(L, JNACL + "crypto_1box_1keypair")(L.env, None, pk.obj, sk.obj)
+    assert pk.mode() == 0 and sk.mode() == 0 and L.fake_outstanding() == 0
+
+
+def test_batch_and_engine_refuse_bad_buffers(shim):
+    L = shim
+    heap = L.fake_heap_buffer()
+    buf = np.zeros(1 << 16, dtype=np.uint8)
+    d = L.fake_direct(buf.ctypes.data, buf.nbytes)
+    short = L.fake_direct(buf.ctypes.data, 39)
+    seal = getattr(L, BATCH + "seal")
+    seal.argtypes = [vp, vp, i64, vp, i32, vp, vp]
+    assert seal(L.env, None, 1, short, 1, d, d) == CZ_EINVAL        # descs shorter than count x 40
+    assert seal(L.env, None, 1, d, 1, heap, d) == CZ_EINVAL         # heap (non-direct) input
+    assert seal(L.env, None, 0, d, 1, d, d) == CZ_EINVAL            # no context
+    su = getattr(L, BATCH + "sealUniform")
+    su.argtypes = [vp, vp, i64, i32, i32, vp, i64, vp, i64, i64, vp, i32]
+    # 4 frames of 100 B at stride 112 into 144-byte slots need 3*112+100 in, 4*144 out
+    assert su(L.env, None, 1, 4, 100, L.fake_direct(buf.ctypes.data, 3 * 112 + 99), 112, d, 144, 3, None, 0) \
+        == CZ_EINVAL
+    assert su(L.env, None, 1, 4, 100, d, 112, L.fake_direct(buf.ctypes.data, 4 * 144 - 1), 144, 3, None, 0) \
+        == CZ_EINVAL
+    assert su(L.env, None, 1, 4, 100, d, 112, d, 144, 3, L.fake_direct(buf.ctypes.data, 3), 0) == CZ_EINVAL
+    ou = getattr(L, BATCH + "openUniform")
+    ou.argtypes = [vp, vp, i64, i32, i32, vp, i64, vp, i64, i64, ctypes.c_uint8, vp, i32]
+    assert ou(L.env, None, 1, 4, 32, d, 144, d, 112, 2, 1, d, 0) == CZ_EINVAL   # size below 33
+    assert ou(L.env, None, 1, 4, 133, d, 144, d, 112, 2, 1, L.fake_direct(buf.ctypes.data, 7), 0) == CZ_EINVAL
+    send = getattr(L, ENGINE + "send")
+    send.argtypes = [vp, vp, i64, i32, vp, i32, i32]
+    assert send(L.env, None, 1, 0, L.fake_direct(buf.ctypes.data, 10), 11, 0) == CZ_EINVAL
+    assert send(L.env, None, 0, 0, d, 10, 0) == CZ_EINVAL
+    ce = getattr(L, ENGINE + "connError")
+    ce.argtypes = [vp, vp, i64, i32, vp]
+    assert ce(L.env, None, 1, 0, Arr(L, np.zeros(0, np.int32), ints=True).obj) == CZ_EINVAL
+    assert getattr(L, ENGINE + "flushOut")(L.env, None, ctypes.c_int64(0)) == CZ_EINVAL
+
+
+def _has_gpu():
+    try:
+        import torch
+        return torch.cuda.is_available()
+    except Exception:
+        return False
+
+
+@pytest.mark.gpu
+def test_jni_seal_open_through_the_shim(shim):
+    """One MESSAGE box through crypto_box_afternm / crypto_box_open_afternm as JeroMQ's Curve.java
+    calls them, in a VM that hands out copies (so a wrong release mode loses the output): the box
+    equals the oracle's MESSAGE body; the open gives back m; a tampered box is -1."""
+    if not _has_gpu():
+        pytest.skip("no GPU")
+    L = shim
+    L.fake_set_copy_mode(1)
+    try:
+        payload = splitmix_bytes(100, 11)
+        m = np.zeros(133, dtype=np.uint8)
+        m[32] = 1                                  # flags byte (MORE)
+        m[33:] = _u8(payload)
+        c, n, k = (Arr(L, np.zeros(133, np.uint8)), Arr(L, _u8(b"CurveZMQMESSAGEC" + (3).to_bytes(8, "big"))),
+                   Arr(L, _u8(PRECOM)))
+        ma = Arr(L, m)
+        assert getattr(L, JNACL + "crypto_1box_1afternm")(L.env, None, c.obj, ma.obj, 133, n.obj, k.obj) == 0
+        body = or_curve_encode(payload, 1, 3, 0, PRECOM)     # "\x07MESSAGE" || nonce[16:24] || box[16:]
+        assert c.np[:16].tobytes() == bytes(16) and c.np[16:].tobytes() == body[16:]
+        back = Arr(L, np.full(133, 0xAA, np.uint8))
+        assert getattr(L, JNACL + "crypto_1box_1open_1afternm")(L.env, None, back.obj, c.obj, 133, n.obj, k.obj) == 0
+        assert back.np[:32].tobytes() == bytes(32) and back.np[32:].tobytes() == m[32:].tobytes()
+        c.np[60] ^= 1
+        assert getattr(L, JNACL + "crypto_1box_1open_1afternm")(L.env, None, back.obj, c.obj, 133, n.obj, k.obj) == -1
+        assert L.fake_outstanding() == 0
+    finally:
+        L.fake_set_copy_mode(0)
+
+
+@pytest.mark.gpu
+def test_jni_batch_and_engine_through_the_shim(shim):
+    """GpuCurveBatch.sealUniform over pinned direct buffers from hostAlloc, and a GpuCurveEngine
+    send -> flushOut -> wireOut, against the oracle."""
+    if not _has_gpu():
+        pytest.skip("no GPU")
+    L = shim
+    create = getattr(L, BATCH + "create")
+    create.argtypes = [vp, vp, i32]
+    ctx = create(L.env, None, 0)
+    assert ctx
+    ha = getattr(L, BATCH + "hostAlloc")
+    ha.argtypes = [vp, vp, i64]
+    count, n, ist, ost = 64, 4096, 4096, 4224
+    bin_, bout, keys = ha(L.env, None, count * ist), ha(L.env, None, count * ost), ha(L.env, None, 32)
+    assert bin_ and bout and keys and L.fake_cap(bin_) == count * ist
+    hin = np.ctypeslib.as_array((ctypes.c_uint8 * (count * ist)).from_address(L.fake_addr(bin_)))
+    hin[:] = _u8(splitmix_bytes(count * ist, 21))
+    ctypes.memmove(L.fake_addr(keys), PRECOM, 32)
+    sk = getattr(L, BATCH + "setKeys")
+    sk.argtypes = [vp, vp, i64, vp, i32, i32]
+    assert sk(L.env, None, ctx, keys, 1, 0) == 0
+    su = getattr(L, BATCH + "sealUniform")
+    su.argtypes = [vp, vp, i64, i32, i32, vp, i64, vp, i64, i64, vp, i32]
+    assert su(L.env, None, ctx, count, n, bin_, ist, bout, ost, 5, None, 0) == 0
+    hout = np.ctypeslib.as_array((ctypes.c_uint8 * (count * ost)).from_address(L.fake_addr(bout)))
+    for i in (0, 31, count - 1):
+        assert hout[i * ost:i * ost + n + 33].tobytes() == or_curve_encode(hin[i * ist:(i + 1) * ist].tobytes(), 0,
+                                                                           5 + i, 0, PRECOM)
+    hf = getattr(L, BATCH + "hostFree")
+    hf.argtypes = [vp, vp, vp]
+    for b in (bin_, bout, keys):
+        hf(L.env, None, b)
+    getattr(L, BATCH + "destroy").argtypes = [vp, vp, i64]
+    getattr(L, BATCH + "destroy")(L.env, None, ctx)
+
+    ec = getattr(L, ENGINE + "create")
+    ec.argtypes = [vp, vp, i64, i32]
+    e = ec(L.env, None, 1 << 20, 0)
+    assert e
+    add = getattr(L, ENGINE + "addConn")
+    add.argtypes = [vp, vp, i64, ctypes.c_uint8, vp, i64, i64]
+    conn = add(L.env, None, e, 0, Arr(L, _u8(PRECOM)).obj, 3, 2)
+    assert conn == 0
+    ma = getattr(L, ENGINE + "msgAlloc")
+    ma.argtypes = [vp, vp, i64, i32]
+    payloads = [splitmix_bytes(sz, 40 + sz) for sz in (0, 100, 5000)]
+    send = getattr(L, ENGINE + "send")
+    send.argtypes = [vp, vp, i64, i32, vp, i32, i32]
+    for j, p in enumerate(payloads):
+        b = ma(L.env, None, e, len(p))
+        assert b and L.fake_cap(b) == len(p)
+        if p:
+            ctypes.memmove(L.fake_addr(b), p, len(p))
+        assert send(L.env, None, e, conn, b, len(p), 1 if j == 0 else 0) == 0
+    getattr(L, ENGINE + "flushOut").argtypes = [vp, vp, i64]
+    assert getattr(L, ENGINE + "flushOut")(L.env, None, e) == 0
+    wo = getattr(L, ENGINE + "wireOut")
+    wo.argtypes = [vp, vp, i64, i32]
+    w = wo(L.env, None, e, conn)
+    got = ctypes.string_at(L.fake_addr(w), L.fake_cap(w))
+    want = b"".join(v2_encode(or_curve_encode(p, 1 if j == 0 else 0, 3 + j, 0, PRECOM)) for j, p in enumerate(payloads))
+    assert got == want
+    wi = getattr(L, ENGINE + "wireIov")
+    wi.argtypes = [vp, vp, i64, i32]
+    arr = wi(L.env, None, e, conn)
+    pieces = [L.fake_elem(arr, i) for i in range(L.fake_len(arr))]
+    assert b"".join(ctypes.string_at(L.fake_addr(p), L.fake_cap(p)) for p in pieces) == want
+    getattr(L, ENGINE + "destroy").argtypes = [vp, vp, i64]
+    getattr(L, ENGINE + "destroy")(L.env, None, e)

@@ -11,6 +11,7 @@
 #include <stdint.h>
 
 #include "cz_salsa_lazy.h"
+#include "cz_salsa_tail.h"
 
 namespace cz {
 
@@ -225,6 +226,63 @@ __device__ __forceinline__ void salsa20_block_frame(u32 x[16], const SalsaFrame 
 #pragma unroll
     for (int i = 0; i < 16; i++)
         x[i] = lazy_pending(i) ? ((x[i] ^ d[i]) + in[i]) : (x[i] + in[i]);
+}
+
+// The last block of a box that uses at most 16 of its bytes (a 100-byte MESSAGE: 133-byte box, 5
+// bytes of block 2): keystream words 0..3 only.  Rounds 3..20 run the tail schedule
+// (cz_salsa_tail.h: the instructions words 0..3 depend on, 692 instead of 736) and the
+// feed-forward covers 4 words; x[4..15] are left unspecified.  The eager path computes the full
+// block and lets the compiler drop what words 0..3 do not need.
+__device__ __forceinline__ void tail_lazy(u32 x[16], u32 d[16])
+{
+#ifdef CZ_SALSA_EAGER
+    rounds_lazy<true>(x, d);
+#else
+    u32 t0, t1, t2, t3;
+    asm(CZ_SALSA_TAIL_ASM
+        : "+v"(x[0]), "+v"(x[1]), "+v"(x[2]), "+v"(x[3]), "+v"(x[4]), "+v"(x[5]), "+v"(x[6]), "+v"(x[7]),
+          "+v"(x[8]), "+v"(x[9]), "+v"(x[10]), "+v"(x[11]), "+v"(x[12]), "+v"(x[13]), "+v"(x[14]), "+v"(x[15]),
+          "=&v"(d[0]), "=&v"(d[1]), "=&v"(d[2]), "=&v"(d[3]), "=&v"(d[4]), "=&v"(d[5]), "=&v"(d[6]), "=&v"(d[7]),
+          "=&v"(d[8]), "=&v"(d[9]), "=&v"(d[10]), "=&v"(d[11]), "=&v"(d[12]), "=&v"(d[13]), "=&v"(d[14]),
+          "=&v"(d[15]), "=&v"(t0), "=&v"(t1), "=&v"(t2), "=&v"(t3));
+#endif
+}
+static_assert(CZ_SALSA_TAIL_WORDS == 4, "tail blocks use keystream words 0..3");
+
+template <bool LAZY = true>
+__device__ __forceinline__ void salsa20_block_w03(u32 x[16], const u32 k[8], u32 n0, u32 n1, u32 c0, u32 c1)
+{
+    const u32 in[16] = {SIGMA0, k[0], k[1], k[2], k[3], SIGMA1, n0, n1, c0, c1, SIGMA2, k[4], k[5], k[6], k[7], SIGMA3};
+#pragma unroll
+    for (int i = 0; i < 16; i++)
+        x[i] = in[i];
+    if constexpr (LAZY) {
+        u32 d[16];
+        col_round(x);
+        row_round(x);
+        tail_lazy(x, d);
+#pragma unroll
+        for (int i = 0; i < 4; i++)
+            x[i] = lazy_pending(i) ? ((x[i] ^ d[i]) + in[i]) : (x[i] + in[i]);
+    } else {
+        rounds_eager(x);
+#pragma unroll
+        for (int i = 0; i < 4; i++)
+            x[i] += in[i];
+    }
+}
+
+__device__ __forceinline__ void salsa20_block_frame_w03(u32 x[16], const SalsaFrame &f, const u32 k[8], u32 n0, u32 n1,
+                                                        u32 c0)
+{
+    const u32 in[4] = {SIGMA0, k[0], k[1], k[2]};
+    u32 d[16];
+    rounds12_frame(x, f, c0, k);
+    tail_lazy(x, d);
+#pragma unroll
+    for (int i = 0; i < 4; i++)
+        x[i] = lazy_pending(i) ? ((x[i] ^ d[i]) + in[i]) : (x[i] + in[i]);
+    (void)n0, (void)n1;
 }
 
 // HSalsa20(k, in16) -> out[8]: no feed-forward, words 0,5,10,15,6,7,8,9.

@@ -643,6 +643,13 @@ __device__ __forceinline__ void seal_frame(const uint8_t *__restrict__ in0, u32 
         else
             salsa20_block<LAZY>(xs, key, n0, n1, c0, c1);
     };
+    // keystream words 0..3 of block c0 only (a last block with <= 16 box bytes)
+    auto ksblock_w03 = [&](u32 *xs, u32 c0) {
+        if constexpr (UN0 && LAZY)
+            salsa20_block_frame_w03(xs, sf, key, n0, n1, c0);
+        else
+            salsa20_block_w03<LAZY>(xs, key, n0, n1, c0, 0u);
+    };
     u32 x[16], C[16];
     ksblock(x, 0u, 0u);
     Poly P;
@@ -713,6 +720,11 @@ __device__ __forceinline__ void seal_frame(const uint8_t *__restrict__ in0, u32 
                     V4 v = ld16f<AL>(src + 16 * c);
                     L[4 * c] = v.x; L[4 * c + 1] = v.y; L[4 * c + 2] = v.z; L[4 * c + 3] = v.w;
                 }
+                // The 8 loads leave together.  Without this fence the scheduler sank each load to just
+                // before its first use inside the two blocks, with a vmcnt(0) behind it: the line was
+                // read in pieces microseconds apart (L2 re-fetched it: FETCH 1.20x the box bytes) and
+                // every load's latency was exposed.
+                __builtin_amdgcn_sched_barrier(0);
                 box_full_block(2u * k, L);
                 box_full_block(2u * k + 1u, L + 16);
                 blk = 2u * k + 2u;
@@ -879,8 +891,30 @@ __device__ __forceinline__ void seal_frame(const uint8_t *__restrict__ in0, u32 
         }
     }
 
-    // final partial block
-    if (tailv != 0 && nfull >= 1) {
+    // final partial block with at most 16 box bytes (a 100-byte MESSAGE's 133-byte box ends 5
+    // bytes into block 2): keystream words 0..3 only, from the tail schedule of rounds 19-20
+    if (tailv != 0 && tailv <= 16u && nfull >= 1) {
+        const u32 blk = nfull;
+        const long o = (MODE == MODE_ZMQ) ? (long)(64u * blk) - 32 : (long)(64u * blk);
+        const V4 q = ldP(in + o, (o >= 0 && (u64)o < inlen) ? inlen - (u64)o : 0);
+        ksblock_w03(x, blk);
+        if constexpr (MODE == MODE_ZMQ) {
+            C[0] = funnel(q.x, carry, sh) ^ x[0];
+            C[1] = funnel(q.y, q.x, sh) ^ x[1];
+            C[2] = funnel(q.z, q.y, sh) ^ x[2];
+            C[3] = funnel(q.w, q.z, sh) ^ x[3];
+        } else {
+            C[0] = q.x ^ x[0]; C[1] = q.y ^ x[1]; C[2] = q.z ^ x[2]; C[3] = q.w ^ x[3];
+        }
+#pragma unroll
+        for (int k = 4; k < 16; k++)
+            C[k] = 0u;
+        if (tailv == 16u)
+            poly_block(P, C[0], C[1], C[2], C[3], 1u);
+        else
+            poly_block_partial(P, C[0], C[1], C[2], C[3], tailv);
+        em.emit(blk, C);
+    } else if (tailv != 0 && nfull >= 1) {
         const u32 blk = nfull;
         V4 q[4];
 #pragma unroll
@@ -1008,6 +1042,14 @@ __device__ __forceinline__ u32 open_frame(const uint8_t *__restrict__ in, u32 si
         else
             salsa20_block<LAZY>(xs, key, n0, n1, c0, c1);
     };
+    // keystream words 0..3 only (a last block holding <= 16 body bytes: 133-byte bodies of 100-byte
+    // MESSAGEs end 5 bytes into block 2); words 4..15 are left unspecified, their bytes masked
+    auto ksblock_w03 = [&](u32 *xs, u32 c0) {
+        if constexpr (UN0 && LAZY)
+            salsa20_block_frame_w03(xs, sf, key, n0, n1, c0);
+        else
+            salsa20_block_w03<LAZY>(xs, key, n0, n1, c0, 0u);
+    };
 
     const u32 mlen = size;
     const u32 nblk = (mlen + 63u) >> 6;
@@ -1096,8 +1138,20 @@ __device__ __forceinline__ u32 open_frame(const uint8_t *__restrict__ in, u32 si
     // load in flight has landed by now (the block's keystream and MAC took ~1000 VALU); say so
     // before the emit, whose line flush issues stores -- vmcnt counts stores too, so otherwise
     // the next block's first use of the pair's second half waits for those stores to complete.
-    auto open_block = [&](u32 blk, bool full, bool drain = false) {
-        ksblock(x, blk, 0u);
+    // Rf (INA 1): the block's 17 raw dwords from the dword-aligned address below it; the byte
+    // funnel into C runs after the keystream, so the wait for the loads comes ~800 VALU after they
+    // were issued (funnelled ahead of the keystream, the loads' latency was exposed per pair)
+    auto open_block = [&](u32 blk, bool full, bool drain = false, const u32 *Rf = nullptr) {
+        if (!full && mlen - 64u * blk <= 16u)
+            ksblock_w03(x, blk);
+        else
+            ksblock(x, blk, 0u);
+        if (Rf) {
+            __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+            for (int q = 0; q < 16; q++)
+                C[q] = funnel(Rf[q + 1], Rf[q], ina);
+        }
         if (full) {
             poly_block(P, C[0], C[1], C[2], C[3], 1u);
             poly_block(P, C[4], C[5], C[6], C[7], 1u);
@@ -1151,6 +1205,7 @@ __device__ __forceinline__ u32 open_frame(const uint8_t *__restrict__ in, u32 si
                 u32 M[32];
                 if constexpr (INA == 1) {
                     // 8 loads from the dword-aligned line below and the dword after it, funnelled
+                    // inside open_block (after the keystream)
                     const uint8_t *src4 = in4 + 128u * k;
                     u32 R[33];
 #pragma unroll
@@ -1159,9 +1214,11 @@ __device__ __forceinline__ u32 open_frame(const uint8_t *__restrict__ in, u32 si
                         R[4 * c] = v.x; R[4 * c + 1] = v.y; R[4 * c + 2] = v.z; R[4 * c + 3] = v.w;
                     }
                     R[32] = ina ? *reinterpret_cast<const u32 *>(src4 + 128) : 0u;  // (2k+2 <= nfull)
-#pragma unroll
-                    for (int q = 0; q < 32; q++)
-                        M[q] = funnel(R[q + 1], R[q], ina);
+                    __builtin_amdgcn_sched_barrier(0);
+                    open_block(2u * k, true, true, R);
+                    open_block(2u * k + 1u, true, false, R + 16);
+                    blk = 2u * k + 2u;
+                    continue;
                 } else {
 #pragma unroll
                     for (int c = 0; c < 8; c++) {

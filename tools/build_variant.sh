@@ -1,6 +1,7 @@
 #!/bin/bash
 # Build an A/B variant of the library: bash tools/build_variant.sh NAME [-DFLAG ...] -> jeromq_amd/libcz_NAME.so
-cd "$(dirname "$0")/../jeromq_amd/csrc" || exit 1
+# (jeromq_amd/build.py: sources compiled in parallel, the linked library gated on the ISA hazard scan)
+cd "$(dirname "$0")/.." || exit 1
 name=$1; shift
-exec /opt/rocm/bin/hipcc --offload-arch=gfx950 -O3 -std=c++17 -fPIC -shared -o ../libcz_$name.so "$@" \
-  cz_kernels.hip cz_x25519.hip cz_host.cpp cz_mechanism.cpp cz_wire.cpp cz_engine.cpp cz_handshake.cpp cz_curve_hs.cpp
+CZ_EXTRA_FLAGS="$*" CZ_LIB_OUT=$PWD/jeromq_amd/libcz_$name.so python3 -c \
+  "from jeromq_amd.build import build_library; build_library(force=True, verbose=False)"

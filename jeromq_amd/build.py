@@ -23,7 +23,7 @@ ROOT = os.path.dirname(HERE)
 CSRC = os.path.join(HERE, "csrc")
 LIB = os.environ.get("CZ_LIB_OUT", os.path.join(HERE, "libcurvezmq_mi355x.so"))
 SOURCES = ["cz_kernels.hip", "cz_x25519.hip", "cz_host.cpp", "cz_mechanism.cpp", "cz_wire.cpp", "cz_engine.cpp", "cz_handshake.cpp", "cz_curve_hs.cpp"]
-HEADERS = ["cz_device.h", "cz_internal.h", "cz_salsa_lazy.h", os.path.join("..", "..", "include", "curvezmq_mi355x.h")]
+HEADERS = ["cz_device.h", "cz_internal.h", "cz_salsa_lazy.h", "cz_salsa_tail.h", os.path.join("..", "..", "include", "curvezmq_mi355x.h")]
 ARCH = os.environ.get("CZ_OFFLOAD_ARCH", "gfx950")
 LLVM_BIN = "/opt/rocm/lib/llvm/bin"
 BUNDLE_MAGIC = b"__CLANG_OFFLOAD_BUNDLE__"
@@ -121,13 +121,15 @@ def build_library(force=False, verbose=True, sources=None, lib=None, src_dir=Non
                 print(" ".join(cmd), file=sys.stderr)
             r = subprocess.run(cmd, cwd=src_dir, capture_output=True, text=True)
             if r.returncode:
+                errs = [ln for ln in r.stderr.splitlines() if "error" in ln][:20]
+                print("\n".join(errs), file=sys.stderr)
                 raise subprocess.CalledProcessError(r.returncode, cmd, r.stdout, r.stderr)
             return obj
         # the largest translation unit first: the kernels dominate the build
         order = sorted(sources, key=lambda f: -os.path.getsize(os.path.join(src_dir, f)))
         with ThreadPoolExecutor(max_workers=jobs or min(len(order), os.cpu_count() or 4, 8)) as ex:
             objs = list(ex.map(compile_one, order))
-        tmp = lib + ".tmp"
+        tmp = f"{lib}.{os.getpid()}.tmp"  # (concurrent builds, e.g. pytest -n, never share a file)
         subprocess.check_call([hipcc, f"--offload-arch={ARCH}", "-shared", "-fPIC", "-o", tmp] + objs, cwd=src_dir)
         try:
             n_co, n_ins = isa_gate(tmp)

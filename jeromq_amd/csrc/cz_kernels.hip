@@ -87,6 +87,11 @@ constexpr int BLOCK = 256;              // threads per workgroup (4 waves)
 #else
 #define CZ_OPEN_UNI_OCC
 #endif
+// k_open_uniform_carry: two aligned lines carried per lane (64 VGPRs) -- 2 waves per SIMD
+#ifndef CZ_OPEN_CARRY_WAVES_PER_EU
+#define CZ_OPEN_CARRY_WAVES_PER_EU 2
+#endif
+#define CZ_OPEN_CARRY_OCC __attribute__((amdgpu_waves_per_eu(CZ_OPEN_CARRY_WAVES_PER_EU, CZ_OPEN_CARRY_WAVES_PER_EU)))
 #ifdef CZ_SEG_WAVES_PER_EU
 #define CZ_SEG_OCC __attribute__((amdgpu_waves_per_eu(CZ_SEG_WAVES_PER_EU, CZ_SEG_WAVES_PER_EU)))
 #else
@@ -249,8 +254,14 @@ __device__ __forceinline__ V4 ld16f(const uint8_t *__restrict__ p)
 // object reaches into it (an aligned 8-byte piece holding a valid byte cannot cross a page).
 __device__ __forceinline__ V4 ld16f_8(const uint8_t *__restrict__ p)
 {
+#ifdef CZ_AL8_X4
+    // one dword-aligned 16-byte load (as the uniform open's INA 8 path) instead of two
+    const uint4 r = *reinterpret_cast<const u4_a4 *>(p);
+    return V4{r.x, r.y, r.z, r.w};
+#else
     const uint2 a = reinterpret_cast<const uint2 *>(p)[0], b = reinterpret_cast<const uint2 *>(p)[1];
     return V4{a.x, a.y, b.x, b.y};
+#endif
 }
 __device__ __forceinline__ V4 ld16_8(const uint8_t *__restrict__ p, u64 avail)
 {
@@ -956,6 +967,39 @@ __device__ __forceinline__ void seal_frame(const uint8_t *__restrict__ in0, u32 
     em.close(false);
 }
 
+// Carry-line input for bodies off 16-byte alignment whose waves share one line phase (the
+// phase-sorted open, k_open_uniform_carry).  A body's pair window k -- its bytes [128k, 128k + 128)
+// plus the dword after, from the dword-aligned address at or below -- is dwords [s, s + 33) of the
+// two aligned 128-byte lines Cur (line k) and Nxt (line k + 1), s = (in4 & 127) / 4 wave-uniform.
+// Each aligned line is loaded once, whole, and carried in registers into the next pair, so no line
+// is read in two parts a pair apart (L2 re-fetched most of them: FETCH 1.84x the body bytes).
+// C[q] = funnel(window[BASE + q + 1], window[BASE + q], ina), q < 16; s selects among 32
+// straight-line cases (wave-uniform branch), each with compile-time register indices.
+template <int S, int BASE>
+__device__ __forceinline__ void carry_window_s(u32 C[16], const u32 Cur[32], const u32 Nxt[32], u32 ina)
+{
+#pragma unroll
+    for (int q = 0; q < 16; q++) {
+        const int lo = BASE + q + S, hi = lo + 1;
+        const u32 vlo = lo < 32 ? Cur[lo & 31] : Nxt[(lo - 32) & 31];
+        const u32 vhi = hi < 32 ? Cur[hi & 31] : Nxt[(hi - 32) & 31];
+        C[q] = funnel(vhi, vlo, ina);
+    }
+}
+template <int BASE>
+__device__ __forceinline__ void carry_window(u32 C[16], const u32 Cur[32], const u32 Nxt[32], u32 s, u32 ina)
+{
+    switch (s) {
+#define CZ_CW(S) case S: carry_window_s<S, BASE>(C, Cur, Nxt, ina); break;
+        CZ_CW(0) CZ_CW(1) CZ_CW(2) CZ_CW(3) CZ_CW(4) CZ_CW(5) CZ_CW(6) CZ_CW(7)
+        CZ_CW(8) CZ_CW(9) CZ_CW(10) CZ_CW(11) CZ_CW(12) CZ_CW(13) CZ_CW(14) CZ_CW(15)
+        CZ_CW(16) CZ_CW(17) CZ_CW(18) CZ_CW(19) CZ_CW(20) CZ_CW(21) CZ_CW(22) CZ_CW(23)
+        CZ_CW(24) CZ_CW(25) CZ_CW(26) CZ_CW(27) CZ_CW(28) CZ_CW(29) CZ_CW(30)
+        default: carry_window_s<31, BASE>(C, Cur, Nxt, ina); break;
+#undef CZ_CW
+    }
+}
+
 // --------------------------------------------------------------------------
 // OPEN one frame.  Returns a CZ_STATUS_* code; the emitter receives the output:
 //   MODE_ZMQ : in = MESSAGE body (size bytes), output = payload (size - 33 bytes);
@@ -973,7 +1017,8 @@ __device__ __forceinline__ void seal_frame(const uint8_t *__restrict__ in0, u32 
 // in & 3 != 0); a whole line is 8 such loads plus that dword.  A chunk whose 16 bytes are all in
 // the body never reads past the dword holding its last byte (a dword cannot cross a page) nor
 // below the body's first dword (the buffer base is dword-aligned).
-template <int MODE, bool AL, class EM, bool PAIR = false, bool UN0 = false, bool LAZY = true, int INA = 16>
+template <int MODE, bool AL, class EM, bool PAIR = false, bool UN0 = false, bool LAZY = true, int INA = 16,
+          bool CARRY = false>
 __device__ __forceinline__ u32 open_frame(const uint8_t *__restrict__ in, u32 size, const u32 key[8],
                                           bool check_floor, long long floor, u32 *flags_out, u64 *nonce_out,
                                           u64 nacl_counter, EM &em)
@@ -1141,7 +1186,8 @@ __device__ __forceinline__ u32 open_frame(const uint8_t *__restrict__ in, u32 si
     // Rf (INA 1): the block's 17 raw dwords from the dword-aligned address below it; the byte
     // funnel into C runs after the keystream, so the wait for the loads comes ~800 VALU after they
     // were issued (funnelled ahead of the keystream, the loads' latency was exposed per pair)
-    auto open_block = [&](u32 blk, bool full, bool drain = false, const u32 *Rf = nullptr) {
+    // fillC (carry path): writes C after the keystream, as Rf does
+    auto open_block_f = [&](u32 blk, bool full, bool drain, const u32 *Rf, auto &&fillC) {
         if (!full && mlen - 64u * blk <= 16u)
             ksblock_w03(x, blk);
         else
@@ -1152,6 +1198,7 @@ __device__ __forceinline__ u32 open_frame(const uint8_t *__restrict__ in, u32 si
             for (int q = 0; q < 16; q++)
                 C[q] = funnel(Rf[q + 1], Rf[q], ina);
         }
+        fillC();
         if (full) {
             poly_block(P, C[0], C[1], C[2], C[3], 1u);
             poly_block(P, C[4], C[5], C[6], C[7], 1u);
@@ -1191,6 +1238,9 @@ __device__ __forceinline__ u32 open_frame(const uint8_t *__restrict__ in, u32 si
             emit_open(blk, X, full);
         }
     };
+    auto open_block = [&](u32 blk, bool full, bool drain = false, const u32 *Rf = nullptr) {
+        open_block_f(blk, full, drain, Rf, [] {});
+    };
 
     u32 blk = 1;
     if constexpr (PAIR && AL) {
@@ -1201,7 +1251,40 @@ __device__ __forceinline__ u32 open_frame(const uint8_t *__restrict__ in, u32 si
                 C[k] = L1[k];  // (loaded with the rest of line 0, above)
             open_block(1, true);
             blk = 2;
-            for (u32 k = 1; 2u * k + 1u < nfull; k++) {
+            if constexpr (CARRY) {
+                static_assert(INA != 16, "carry-line input is for bodies off 16-byte alignment");
+                // the caller sorted frames so that every lane of the wave has the same line phase
+                const uint8_t *lb = reinterpret_cast<const uint8_t *>((uintptr_t)in4 & ~(uintptr_t)127);
+                const u32 s = __builtin_amdgcn_readfirstlane(((u32)(uintptr_t)in4 & 127u) >> 2);
+                u32 Cur[32], Nxt[32];
+                auto load_line = [&](u32 *D, const uint8_t *p) {
+#pragma unroll
+                    for (int c = 0; c < 8; c++) {
+                        const uint4 v = *reinterpret_cast<const uint4 *>(p + 16 * c);
+                        D[4 * c] = v.x; D[4 * c + 1] = v.y; D[4 * c + 2] = v.z; D[4 * c + 3] = v.w;
+                    }
+                };
+                // aligned line 1 (window 0 above read its first s + 1 dwords a moment ago)
+                load_line(Cur, lb + 128);
+                for (u32 k = 1; 2u * k + 1u < nfull; k++) {
+                    // aligned line k + 1: it holds a body byte (2k + 2 <= nfull), so it is mapped
+                    load_line(Nxt, lb + 128u * (k + 1u));
+                    __builtin_amdgcn_sched_barrier(0);
+                    open_block_f(2u * k, true, true, nullptr, [&] {
+                        __builtin_amdgcn_sched_barrier(0);
+                        carry_window<0>(C, Cur, Nxt, s, ina);
+                    });
+                    open_block_f(2u * k + 1u, true, false, nullptr, [&] {
+                        __builtin_amdgcn_sched_barrier(0);
+                        carry_window<16>(C, Cur, Nxt, s, ina);
+                    });
+#pragma unroll
+                    for (int q = 0; q < 32; q++)
+                        Cur[q] = Nxt[q];
+                    blk = 2u * k + 2u;
+                }
+            }
+            for (u32 k = 1; !CARRY && 2u * k + 1u < nfull; k++) {
                 u32 M[32];
                 if constexpr (INA == 1) {
                     // 8 loads from the dword-aligned line below and the dword after it, funnelled
@@ -2407,8 +2490,11 @@ __global__ __launch_bounds__(BLOCK) CZ_OCC CZ_OPEN_UNI_OCC void k_open_uniform(c
                                                          uint8_t *__restrict__ out, uint64_t out_stride,
                                                          uint32_t count, uint32_t size,
                                                          const uint8_t *__restrict__ subkey, uint64_t floor0,
-                                                         int check, uint16_t *__restrict__ status, int allow_un0)
+                                                         int check, uint16_t *__restrict__ status, int allow_un0,
+                                                         int prev0 = 0)
 {
+    // prev0: frame 0's floor is the nonce of the body in_stride bytes before it (a tail launched
+    // behind the phase-sorted carry kernel), not floor0
     static_assert(INA == 16 || ST != ST_DIRECT, "unaligned bodies: staged plaintext only");
     extern __shared__ uint4 smem[];
     uint32_t i = blockIdx.x * BLOCK + threadIdx.x;
@@ -2433,7 +2519,7 @@ __global__ __launch_bounds__(BLOCK) CZ_OCC CZ_OPEN_UNI_OCC void k_open_uniform(c
     if (ST != ST_DIRECT && full_wave) {
         // (16-byte aligned slots here: the previous body's nonce is one 8-byte load, not 8 byte loads)
         long long floor = (long long)floor0;
-        if (i > 0) {
+        if (i > 0 || prev0) {
             if constexpr (INA >= 8) {
                 const uint2 pn = *reinterpret_cast<const uint2 *>(src - in_stride + 8);
                 floor = (long long)(((u64)bswap32(pn.x) << 32) | (u64)bswap32(pn.y));
@@ -2480,7 +2566,7 @@ __global__ __launch_bounds__(BLOCK) CZ_OCC CZ_OPEN_UNI_OCC void k_open_uniform(c
     }
     if (i >= count)
         return;
-    long long floor = i > 0 ? (long long)read_be64(src - in_stride + 8) : (long long)floor0;
+    long long floor = (i > 0 || prev0) ? (long long)read_be64(src - in_stride + 8) : (long long)floor0;
     if (aligned16(src, dst)) {
         EmitDirect<true> em{dst, nout};
         st = open_frame<MODE_ZMQ, true>(src, size, key, check != 0, floor, &fl, &nonce, 0, em);
@@ -2491,6 +2577,55 @@ __global__ __launch_bounds__(BLOCK) CZ_OCC CZ_OPEN_UNI_OCC void k_open_uniform(c
     status[i] = (uint16_t)(st | (st == CZ_STATUS_OK ? (fl << 8) : 0u));
 }
 
+// Phase-sorted open of bodies off 16-byte alignment into line-aligned plaintext slots (the dense
+// wire layout: V2Decoder leaves bodies back to back, zmq/io/coder/v2/V2Decoder.java:67-105).
+// Frame i's body starts (in + i * in_stride) & 127 bytes into a cache line; that phase repeats
+// every P = 128 / gcd(in_stride mod 128, 128) frames.  Within each block of 64 P frames, wave c
+// takes frames c, c + P, ..., c + 63 P: one phase per wave, so open_frame<CARRY> loads every
+// aligned line of a body once and carries it into the next pair.  Plaintext slot j of the wave is
+// out + (first + P j) * out_stride, EmitLines with a lane stride of P * out_stride.  nwaves = the
+// number of whole blocks x P; the frames after them go to k_open_uniform (prev0 = 1).
+template <int INA>
+__global__ __launch_bounds__(BLOCK) CZ_OPEN_CARRY_OCC void k_open_uniform_carry(
+    const uint8_t *__restrict__ in, uint64_t in_stride, uint8_t *__restrict__ out, uint64_t out_stride, uint32_t nwaves,
+    uint32_t P, uint32_t size, const uint8_t *__restrict__ subkey, uint64_t floor0, int check,
+    uint16_t *__restrict__ status, int allow_un0)
+{
+    extern __shared__ uint4 smem[];
+    const uint32_t w = (blockIdx.x * BLOCK + threadIdx.x) >> 6;
+    if (w >= nwaves)
+        return;
+    const u32 lane = threadIdx.x & 63u;
+    const uint32_t first = (w / P) * 64u * P + w % P;
+    const uint32_t i = first + P * lane;
+    u32 key[8];
+    load_key(subkey, key);
+    const uint8_t *src = in + (uint64_t)i * in_stride;
+    uint8_t *dst = out + (uint64_t)i * out_stride;
+    const u32 nout = size - 33u;
+    long long floor = (long long)floor0;
+    if (i > 0) {
+        if constexpr (INA >= 8) {
+            const uint2 pn = *reinterpret_cast<const uint2 *>(src - in_stride + 8);
+            floor = (long long)(((u64)bswap32(pn.x) << 32) | (u64)bswap32(pn.y));
+        } else {
+            floor = (long long)read_be64(src - in_stride + 8);
+        }
+    }
+    const bool un0 = allow_un0 && wave_uniform(INA >= 8 ? *reinterpret_cast<const u32 *>(src + 8) : ld32<false>(src + 8));
+    EmitLines em{smem + (threadIdx.x >> 6) * (LINE_LDS_BYTES / 16), out + (uint64_t)first * out_stride, dst,
+                 (uint64_t)P * out_stride, lane, nout, 0u, false};
+    u32 fl = 0;
+    u64 nonce = 0;
+    u32 st;
+    if (un0)
+        st = open_frame<MODE_ZMQ, true, EmitLines, true, true, true, INA, true>(src, size, key, check != 0, floor, &fl,
+                                                                            &nonce, 0, em);
+    else
+        st = open_frame<MODE_ZMQ, true, EmitLines, true, false, true, INA, true>(src, size, key, check != 0, floor, &fl,
+                                                                             &nonce, 0, em);
+    status[i] = (uint16_t)(st | (st == CZ_STATUS_OK ? (fl << 8) : 0u));
+}
 
 // ---- segmented (ragged) batches ------------------------------------------
 constexpr int SEGMODE_LINES = 1;  // line-staged stores for waves of equal-length segments
@@ -3218,6 +3353,7 @@ static int g_seglines = 1;  // line-staged stores for waves of equal-length segm
 static int g_shift = 1;     // uniform seal: shifted line staging for bodies at any byte offset
 static int g_open_ina = 1;  // uniform open: line path for bodies off 16-byte alignment (dword-aligned loads)
 static int g_seal_ina = 1;  // seal: staged / line paths for payloads off 16-byte alignment
+static int g_open_carry = 0;  // uniform open off 16-byte alignment: phase-sorted waves, carried lines (A/B pending)
 // segment kernels: waves of 16-byte aligned outputs that are not all on 128-byte lines go through
 // EmitShiftLines (whole cache lines) instead of EmitSegLines (128-byte groups at each output's
 // base, two partial cache lines per group): Zipf seal with 16-byte output slots 1250 -> 1629 GiB/s
@@ -3353,11 +3489,11 @@ hipError_t czk_open_uniform(const void *in, uint64_t in_stride, void *out, uint6
     const uint32_t nout = size >= 33u ? size - 33u : 0u;
 #define CZ_OPEN_LAUNCH(ST, PR, LDS)                                                                        \
     hipLaunchKernelGGL((k_open_uniform<ST, PR>), grid, dim3(BLOCK), (LDS), s, (const uint8_t *)in, in_stride,   \
-                       (uint8_t *)out, out_stride, count, size, (const uint8_t *)subkey, floor0, check, status, g_un0)
+                       (uint8_t *)out, out_stride, count, size, (const uint8_t *)subkey, floor0, check, status, g_un0, 0)
 #define CZ_OPEN_LAUNCH_INA(ST, INA, LDS)                                                                     \
     hipLaunchKernelGGL((k_open_uniform<ST, true, INA>), grid, dim3(BLOCK), (LDS), s, (const uint8_t *)in,          \
                        in_stride, (uint8_t *)out, out_stride, count, size, (const uint8_t *)subkey, floor0, check, \
-                       status, g_un0)
+                       status, g_un0, 0)
     const int st = size >= 33u ? pick_staging(out_stride, nout, al) : (int)ST_DIRECT;
     const unsigned lds = st == ST_LINES ? WAVES * LINE_LDS_BYTES : (st == ST_REGION ? (unsigned)(WAVES * 64 * out_stride) : 0u);
     // bodies off 16-byte alignment (the dense wire layout) into line-aligned plaintext slots: the
@@ -3376,12 +3512,55 @@ hipError_t czk_open_uniform(const void *in, uint64_t in_stride, void *out, uint6
         if (ina == 8)
             hipLaunchKernelGGL((k_open_uniform<ST_REGION, false, 8>), grid, dim3(BLOCK), lds_out_region, s,
                                (const uint8_t *)in, in_stride, (uint8_t *)out, out_stride, count, size,
-                               (const uint8_t *)subkey, floor0, check, status, g_un0);
+                               (const uint8_t *)subkey, floor0, check, status, g_un0, 0);
         else
             hipLaunchKernelGGL((k_open_uniform<ST_REGION, false, 1>), grid, dim3(BLOCK), lds_out_region, s,
                                (const uint8_t *)in, in_stride, (uint8_t *)out, out_stride, count, size,
-                               (const uint8_t *)subkey, floor0, check, status, g_un0);
+                               (const uint8_t *)subkey, floor0, check, status, g_un0, 0);
         return hipGetLastError();
+    }
+    if (g_pair && st_out == ST_LINES && ina != 16 && g_open_ina && g_open_carry && nout >= 256u) {
+        // phase-sorted waves with carried aligned lines (k_open_uniform_carry): whole blocks of 64 P
+        // frames, P = the period of the bodies' line phase; the rest through k_open_uniform
+        uint64_t g = in_stride & 127u, m = 128u;
+        while (g) {  // gcd(in_stride mod 128, 128)
+            const uint64_t t = m % g;
+            m = g;
+            g = t;
+        }
+        const uint32_t P = (uint32_t)(128u / m);
+        const uint64_t blocks = count / (64ull * P);
+        if (blocks > 0 && 64ull * P * out_stride < (1ull << 31)) {
+            const uint32_t nwaves = (uint32_t)(blocks * P);
+            const dim3 cgrid((nwaves + WAVES - 1) / WAVES);
+            if (ina == 8)
+                hipLaunchKernelGGL((k_open_uniform_carry<8>), cgrid, dim3(BLOCK), WAVES * LINE_LDS_BYTES, s,
+                                   (const uint8_t *)in, in_stride, (uint8_t *)out, out_stride, nwaves, P, size,
+                                   (const uint8_t *)subkey, floor0, check, status, g_un0);
+            else
+                hipLaunchKernelGGL((k_open_uniform_carry<1>), cgrid, dim3(BLOCK), WAVES * LINE_LDS_BYTES, s,
+                                   (const uint8_t *)in, in_stride, (uint8_t *)out, out_stride, nwaves, P, size,
+                                   (const uint8_t *)subkey, floor0, check, status, g_un0);
+            const uint64_t done = blocks * 64ull * P;
+            if (done < count) {
+                hipError_t e = hipGetLastError();
+                if (e != hipSuccess)
+                    return e;
+                const uint32_t rest = count - (uint32_t)done;
+                const dim3 tgrid((rest + BLOCK - 1) / BLOCK);
+                const uint8_t *tin = (const uint8_t *)in + done * in_stride;
+                uint8_t *tout = (uint8_t *)out + done * out_stride;
+                if (ina == 8)
+                    hipLaunchKernelGGL((k_open_uniform<ST_LINES, true, 8>), tgrid, dim3(BLOCK), WAVES * LINE_LDS_BYTES,
+                                       s, tin, in_stride, tout, out_stride, rest, size, (const uint8_t *)subkey, floor0,
+                                       check, status + done, g_un0, 1);
+                else
+                    hipLaunchKernelGGL((k_open_uniform<ST_LINES, true, 1>), tgrid, dim3(BLOCK), WAVES * LINE_LDS_BYTES,
+                                       s, tin, in_stride, tout, out_stride, rest, size, (const uint8_t *)subkey, floor0,
+                                       check, status + done, g_un0, 1);
+            }
+            return hipGetLastError();
+        }
     }
     if (g_pair && (st_out == ST_SHIFT || (st_out == ST_LINES && ina != 16)) && (ina == 16 || g_open_ina)) {
         if (st_out == ST_LINES) {
@@ -3530,6 +3709,11 @@ int czk_tune(const char *key, int value)
     if (__builtin_strcmp(key, "open_ina") == 0) {
         int old = g_open_ina;
         g_open_ina = value != 0;
+        return old;
+    }
+    if (__builtin_strcmp(key, "open_carry") == 0) {
+        int old = g_open_carry;
+        g_open_carry = value != 0;
         return old;
     }
     if (__builtin_strcmp(key, "shift16") == 0) {

@@ -244,3 +244,66 @@ def test_seal_uniform_unaligned_payloads(torch_dev, subkeys, n, in_stride, out_s
         want = or_curve_encode(p, int(fl[i]), c0 + i, 0, PRECOM)
         assert out[i * out_stride:i * out_stride + n + 33].tobytes() == want, \
             f"frame {i} (in_stride {in_stride}, out_stride {out_stride}, ibase {ibase})"
+
+
+@pytest.mark.parametrize("n,stride,base,tail", [(4096, 4129, 0, 37), (4096, 4129, 3, 0), (1024, 1064, 8, 21),
+                                                (4096, 4136, 8, 5), (512, 545, 1, 64 * 3 + 1), (2048, 2050, 2, 9)])
+@pytest.mark.parametrize("carry", [1, 0])
+def test_open_uniform_phase_sorted_carry(torch_dev, subkeys, n, stride, base, tail, carry):
+    """The phase-sorted open of bodies off 16-byte alignment (k_open_uniform_carry, cz_tune
+    "open_carry"): whole blocks of 64 P frames, P = the period of the bodies' line phase (128 for a
+    4129-byte stride, 16 for 4136 or 1064, 64 for 2050), every wave one phase with the aligned lines
+    carried; the frames after the last whole block go to k_open_uniform, whose first frame takes its
+    replay floor from the body before it.  Tampered frames inside carry waves and in the tail report
+    CRYPTO with zeros; a replayed nonce on the first tail frame reports SEQUENCE; every other payload
+    and flags byte comes back, with carry on and off."""
+    torch, dev = torch_dev
+    from jeromq_amd import _lib, batch
+    g = np.gcd(stride % 128, 128) if stride % 128 else 128
+    P = 128 // g
+    count = 64 * P + tail
+    in_stride = (n + 15) // 16 * 16
+    hin = np.frombuffer(splitmix_bytes(count * in_stride, 3000 + n + stride), dtype=np.uint8).copy()
+    d_in = torch.from_numpy(hin).to(dev)
+    d_buf = torch.full((base + count * stride + 64,), SENTINEL, dtype=torch.uint8, device=dev)
+    d_bodies = d_buf[base:]
+    flags = torch.tensor([(i % 3 == 0) for i in range(count)], dtype=torch.uint8, device=dev)
+    c0 = 0xFFFFFFF0 - 1000  # the high nonce word changes inside the batch
+    batch.seal_uniform(d_in, in_stride, d_bodies, stride, count, n, subkeys[0], c0, flags8=flags)
+    torch.cuda.synchronize()
+    bodies = d_buf.cpu().numpy()
+    rng = np.random.default_rng(n + stride + base)
+    bad = sorted(set(int(x) for x in rng.choice(64 * P, size=7, replace=False)) | ({64 * P + tail // 2} if tail > 2 else set()))
+    for j, i in enumerate(bad):  # tag, first / middle / last ciphertext byte
+        where = [16 + j % 16, 33, (n + 33) // 2, n + 32][j % 4]
+        bodies[base + i * stride + where] ^= 1 << (j % 8)
+    replay = 64 * P if tail else None
+    if replay is not None:   # the first tail frame repeats the nonce of the last carry frame
+        o, p = base + replay * stride, base + (replay - 1) * stride
+        bodies[o + 8:o + 16] = bodies[p + 8:p + 16]
+    d_buf.copy_(torch.from_numpy(bodies))
+    plain_stride = (n + 127) // 128 * 128
+    d_plain = torch.full((count * plain_stride + 64,), SENTINEL, dtype=torch.uint8, device=dev)
+    status = torch.full((count,), -1, dtype=torch.int16, device=dev)
+    lib = _lib.lib()
+    old = lib.cz_tune(b"open_carry", carry)
+    try:
+        batch.open_uniform(d_bodies, stride, d_plain, plain_stride, count, n + 33, subkeys[0], c0 - 1, status)
+        torch.cuda.synchronize()
+    finally:
+        lib.cz_tune(b"open_carry", old)
+    st = status.cpu().numpy().view(np.uint16)
+    plain = d_plain.cpu().numpy()
+    fl = flags.cpu().numpy()
+    for i in range(count):
+        p = plain[i * plain_stride:i * plain_stride + n]
+        if i in bad:
+            assert st[i] & 0xff == _lib.CZ_STATUS_CRYPTO, f"frame {i} status {st[i]:#x}"
+            assert not p.any(), f"frame {i} leaked plaintext"
+        elif i == replay:
+            assert st[i] & 0xff == _lib.CZ_STATUS_SEQUENCE, f"replayed frame {i} status {st[i]:#x}"
+            assert not p.any(), f"frame {i} leaked plaintext"
+        else:
+            assert st[i] & 0xff == _lib.CZ_STATUS_OK and st[i] >> 8 == fl[i], f"frame {i} status {st[i]:#x}"
+            assert p.tobytes() == hin[i * in_stride:i * in_stride + n].tobytes(), f"frame {i}"
+        assert not plain[i * plain_stride + n:(i + 1) * plain_stride].any(), f"slot {i} padding"

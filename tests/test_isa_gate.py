@@ -39,7 +39,7 @@ def test_gate_refuses_register_soffset_store(tmp_path):
     build, lib, run = _build(tmp_path, "soff")
     with pytest.raises(build.IsaHazardError, match="register soffset"):
         run()
-    assert not os.path.exists(lib) and not os.path.exists(lib + ".tmp")
+    assert not os.path.exists(lib) and not [f for f in os.listdir(tmp_path) if f.endswith(".tmp")]
 
 
 @needs_hipcc

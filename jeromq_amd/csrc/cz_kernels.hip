@@ -98,7 +98,11 @@ constexpr int BLOCK = 256;              // threads per workgroup (4 waves)
 #define CZ_SEG_OCC
 #endif
 constexpr int WAVES = BLOCK / 64;
+#ifdef CZ_FLUSH2
+constexpr u32 LINE_LDS_BYTES = 64 * 256; // EmitLines2 (A/B build): two 128-byte lines per frame
+#else
 constexpr u32 LINE_LDS_BYTES = 64 * 128; // EmitLines: one 128-byte line per frame
+#endif
 constexpr u32 HOLD_LDS_BYTES = 64 * 64;  // EmitLines (seal): block 1 of every frame, until tag()
 constexpr u32 REGION_MAX = 16384;       // EmitRegion: 64 slots per wave
 
@@ -523,6 +527,136 @@ struct EmitLines {
     }
 };
 
+#ifdef CZ_FLUSH2
+// A/B build only (-DCZ_FLUSH2, DESIGN.md section 6, "the write-path clock"): EmitLines for the
+// seal with TWO lines per store instruction.  Rows are 256 bytes (16 units) per frame, a flush
+// every 4 chunks stores lines 2lp and 2lp+1 of the 64 frames as 16 global_store_dwordx4 of 4
+// frames x 256 bytes (EmitLines: 8 instructions of 8 frames x 128 bytes every 2 chunks).  Line 0
+// still leaves whole with the tag from close() (single-line store).  16 KiB of LDS per wave: 2 waves
+// per SIMD.
+struct EmitLines2 {
+    static constexpr bool cooperative = true;
+    uint4 *lds;        // this wave's 64 x 16 units
+    uint8_t *wbase;
+    uint8_t *mine;
+    u64 stride;
+    u32 lane, total, last_q;
+    bool tag_slot;
+    uint4 *hold;
+    u32 head[12];
+    u32 tagw[4];
+
+    // lines 2lp (first) and / or 2lp+1 (second) of the wave's 64 frames
+    __device__ __forceinline__ void flush_pair(u32 lp, bool first, bool second)
+    {
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // the other lanes' ds_writes of these lines
+        const u64 base = uniform64((u64)(uintptr_t)wbase) + 256ull * lp;
+        if (first && second) {
+            const u32 u = lane & 15u, r = lane >> 4;
+            const u32 voff = r * (u32)stride + 16u * u;
+            const u32 step = 4u * (u32)stride;
+#pragma unroll
+            for (u32 j = 0; j < 16; j++) {
+                const u32 F = 4u * j + r;
+                buf_store16(base + (u64)(j * step), voff, lds[F * 16u + (u ^ (F & 15u))]);
+            }
+        } else {
+            const u32 half = first ? 0u : 1u;
+            const u32 c = lane & 7u, r = lane >> 3;
+            const u32 voff = r * (u32)stride + 16u * c;
+            const u32 step = 8u * (u32)stride;
+#pragma unroll
+            for (u32 j = 0; j < 8; j++) {
+                const u32 F = 8u * j + r;
+                buf_store16(base + 128ull * half + (u64)(j * step), voff, lds[F * 16u + ((8u * half + c) ^ (F & 15u))]);
+            }
+        }
+    }
+    __device__ __forceinline__ void emit(u32 q, const u32 Din[16])
+    {
+        u32 D[16];
+#pragma unroll
+        for (int k = 0; k < 16; k++)
+            D[k] = Din[k];
+        if (64u * q + 64u > total)
+            mask_chunk(D, total > 64u * q ? total - 64u * q : 0u);
+        emit_full(q, D);
+    }
+    __device__ __forceinline__ void emit_full(u32 q, const u32 D[16])
+    {
+        if (tag_slot && q == 0u) {
+#pragma unroll
+            for (int k = 0; k < 4; k++)
+                head[k] = D[k];
+#pragma unroll
+            for (int k = 0; k < 8; k++)
+                head[4 + k] = D[8 + k];
+        }
+        if (tag_slot && q == 1u) {
+#pragma unroll
+            for (u32 c = 0; c < 4; c++)
+                hold[lane * 4u + c] = make_uint4(D[4 * c], D[4 * c + 1], D[4 * c + 2], D[4 * c + 3]);
+        }
+        const u32 pos = 4u * (q & 3u);
+        const u32 sw = lane & 15u;
+#pragma unroll
+        for (u32 c = 0; c < 4; c++)
+            lds[lane * 16u + ((pos + c) ^ sw)] = make_uint4(D[4 * c], D[4 * c + 1], D[4 * c + 2], D[4 * c + 3]);
+        if ((q & 3u) == 3u)
+            flush_pair(q >> 2, !(tag_slot && q == 3u), true);
+        last_q = q;
+    }
+    __device__ __forceinline__ void tag(const u32 t[4])
+    {
+#pragma unroll
+        for (int k = 0; k < 4; k++)
+            tagw[k] = t[k];
+    }
+    __device__ __forceinline__ void line0()
+    {
+        const u32 sw = lane & 15u;
+        const bool one = last_q == 0u;
+        uint4 b1[4];
+#pragma unroll
+        for (u32 c = 0; c < 4; c++)
+            b1[c] = one ? make_uint4(0u, 0u, 0u, 0u) : hold[lane * 4u + c];
+        lds[lane * 16u + (0u ^ sw)] = make_uint4(head[0], head[1], head[2], head[3]);
+        lds[lane * 16u + (1u ^ sw)] = make_uint4(tagw[0], tagw[1], tagw[2], tagw[3]);
+        lds[lane * 16u + (2u ^ sw)] = make_uint4(head[4], head[5], head[6], head[7]);
+        lds[lane * 16u + (3u ^ sw)] = make_uint4(head[8], head[9], head[10], head[11]);
+#pragma unroll
+        for (u32 c = 0; c < 4; c++)
+            lds[lane * 16u + ((4u + c) ^ sw)] = b1[c];
+        flush_pair(0, true, false);
+    }
+    // the last pair when it did not end on a 4-chunk boundary: zero the rest of the row and store
+    // the lines that hold chunks (the line of the last chunk is the slot's last written line, as
+    // in EmitLines)
+    __device__ __forceinline__ void finish()
+    {
+        const u32 r = last_q & 3u;
+        if (r == 3u)
+            return;
+        const u32 sw = lane & 15u;
+        const u32 done = 4u * (r + 1u), end = r < 2u ? 8u : 16u;
+        for (u32 u = done; u < end; u++)
+            lds[lane * 16u + (u ^ sw)] = make_uint4(0u, 0u, 0u, 0u);
+        const u32 lp = last_q >> 2;
+        const bool first = !(tag_slot && lp == 0u);
+        const bool second = r >= 2u;
+        if (first || second)
+            flush_pair(lp, first, second);
+    }
+    __device__ __forceinline__ void close(bool bad)
+    {
+        (void)bad;  // seal only
+        finish();
+        if (tag_slot)
+            line0();
+    }
+};
+#endif
+
 // Whole-region staging for a full wave of small equal-length frames: the wave's
 // 64 slots (64 * stride <= REGION_MAX, stride % 16 == 0) are assembled in LDS
 // and written with contiguous 1 KiB store instructions.  Slot bytes beyond
@@ -731,11 +865,10 @@ __device__ __forceinline__ void seal_frame(const uint8_t *__restrict__ in0, u32 
                     V4 v = ld16f<AL>(src + 16 * c);
                     L[4 * c] = v.x; L[4 * c + 1] = v.y; L[4 * c + 2] = v.z; L[4 * c + 3] = v.w;
                 }
-                // The 8 loads leave together.  Without this fence the scheduler sank each load to just
-                // before its first use inside the two blocks, with a vmcnt(0) behind it: the line was
-                // read in pieces microseconds apart (L2 re-fetched it: FETCH 1.20x the box bytes) and
-                // every load's latency was exposed.
-                __builtin_amdgcn_sched_barrier(0);
+                // (The scheduler sinks each of these loads to just before its first use, with a vmcnt(0)
+                // behind it, so a line is read in pieces and L2 re-fetches it: FETCH 1.20x the box
+                // bytes.  A sched_barrier here keeps the 8 loads together and the first wait ~1570
+                // instructions later -- and measured 14% SLOWER (interleaved A/B).)
                 box_full_block(2u * k, L);
                 box_full_block(2u * k + 1u, L + 16);
                 blk = 2u * k + 2u;
@@ -2352,13 +2485,18 @@ __device__ __forceinline__ void seal_uniform_body(const uint8_t *__restrict__ in
         const u32 fl = (MODE == MODE_ZMQ && flags8) ? flags8[i] : 0u;
         const u32 lane = threadIdx.x & 63u;
         if constexpr (ST == ST_LINES) {
-            EmitLines em{smem + (threadIdx.x >> 6) * (LINE_LDS_BYTES / 16), out + (uint64_t)wave_first * out_stride,
-                         dst, out_stride, lane, mlen, 0u, true,
-                         smem + (WAVES * LINE_LDS_BYTES + (threadIdx.x >> 6) * HOLD_LDS_BYTES) / 16};
+#ifdef CZ_FLUSH2
+            using EmL = EmitLines2;
+#else
+            using EmL = EmitLines;
+#endif
+            EmL em{smem + (threadIdx.x >> 6) * (LINE_LDS_BYTES / 16), out + (uint64_t)wave_first * out_stride,
+                   dst, out_stride, lane, mlen, 0u, true,
+                   smem + (WAVES * LINE_LDS_BYTES + (threadIdx.x >> 6) * HOLD_LDS_BYTES) / 16};
             if (un0)
-                seal_frame<MODE, true, EmitLines, PAIR, true, true, INA>(src, len, fl, counter0 + i, key, em);
+                seal_frame<MODE, true, EmL, PAIR, true, true, INA>(src, len, fl, counter0 + i, key, em);
             else
-                seal_frame<MODE, true, EmitLines, PAIR, false, true, INA>(src, len, fl, counter0 + i, key, em);
+                seal_frame<MODE, true, EmL, PAIR, false, true, INA>(src, len, fl, counter0 + i, key, em);
         } else if constexpr (ST == ST_SHIFT) {
             // bodies at any byte offset (dense packing, wire layout): byte-shifted line staging
             EmitShiftLinesUni em{reinterpret_cast<uint8_t *>(smem) + (threadIdx.x >> 6) * SHIFT_LDS_BYTES, dst, lane,
@@ -2393,6 +2531,10 @@ __device__ __forceinline__ void seal_uniform_body(const uint8_t *__restrict__ in
         EmitDirect<false> em{dst, mlen};
         seal_frame<MODE, false>(src, len, fl, counter0 + i, key, em);
     }
+    // the partial last wave of a batch that owns its slots: zeros past the body, as the staged waves
+    if constexpr (ST == ST_LINES || ST == ST_REGION)
+        if (out_stride > mlen)
+            zero_bytes(dst + mlen, (u32)(out_stride - mlen));
 }
 
 template <int ST, bool PAIR, int MODE = MODE_ZMQ>
@@ -2574,6 +2716,15 @@ __global__ __launch_bounds__(BLOCK) CZ_OCC CZ_OPEN_UNI_OCC void k_open_uniform(c
         EmitDirect<false> em{dst, nout};
         st = open_frame<MODE_ZMQ, false>(src, size, key, check != 0, floor, &fl, &nonce, 0, em);
     }
+    // lane-wise frames (a partial last wave, or a batch the staged emitters do not take) keep the
+    // staged waves' contract: zeros in the payload of a frame rejected before decryption, which
+    // emitted nothing (a bad tag's plaintext was already zeroed by poison()), and, in a batch that
+    // owns its slots, zeros past the payload
+    if (st != CZ_STATUS_OK && st != CZ_STATUS_CRYPTO)
+        zero_bytes(dst, nout);
+    if constexpr (ST == ST_LINES || ST == ST_REGION)
+        if (out_stride > nout)
+            zero_bytes(dst + nout, (u32)(out_stride - nout));
     status[i] = (uint16_t)(st | (st == CZ_STATUS_OK ? (fl << 8) : 0u));
 }
 
@@ -3353,7 +3504,10 @@ static int g_seglines = 1;  // line-staged stores for waves of equal-length segm
 static int g_shift = 1;     // uniform seal: shifted line staging for bodies at any byte offset
 static int g_open_ina = 1;  // uniform open: line path for bodies off 16-byte alignment (dword-aligned loads)
 static int g_seal_ina = 1;  // seal: staged / line paths for payloads off 16-byte alignment
-static int g_open_carry = 0;  // uniform open off 16-byte alignment: phase-sorted waves, carried lines (A/B pending)
+#ifndef CZ_OPEN_CARRY_DEFAULT
+#define CZ_OPEN_CARRY_DEFAULT 1
+#endif
+static int g_open_carry = CZ_OPEN_CARRY_DEFAULT;  // uniform open off 16-byte alignment: phase-sorted waves, carried lines
 // segment kernels: waves of 16-byte aligned outputs that are not all on 128-byte lines go through
 // EmitShiftLines (whole cache lines) instead of EmitSegLines (128-byte groups at each output's
 // base, two partial cache lines per group): Zipf seal with 16-byte output slots 1250 -> 1629 GiB/s
@@ -3519,7 +3673,9 @@ hipError_t czk_open_uniform(const void *in, uint64_t in_stride, void *out, uint6
                                (const uint8_t *)subkey, floor0, check, status, g_un0, 0);
         return hipGetLastError();
     }
-    if (g_pair && st_out == ST_LINES && ina != 16 && g_open_ina && g_open_carry && nout >= 256u) {
+    // (INA 1 -- any byte offset -- measured 1.3% slower with carried lines at 2 waves per SIMD than
+    // the straddling loads at 3, so only 8-byte aligned bodies take it: +2.6%)
+    if (g_pair && st_out == ST_LINES && ina == 8 && g_open_ina && g_open_carry && nout >= 256u) {
         // phase-sorted waves with carried aligned lines (k_open_uniform_carry): whole blocks of 64 P
         // frames, P = the period of the bodies' line phase; the rest through k_open_uniform
         uint64_t g = in_stride & 127u, m = 128u;
@@ -3533,14 +3689,9 @@ hipError_t czk_open_uniform(const void *in, uint64_t in_stride, void *out, uint6
         if (blocks > 0 && 64ull * P * out_stride < (1ull << 31)) {
             const uint32_t nwaves = (uint32_t)(blocks * P);
             const dim3 cgrid((nwaves + WAVES - 1) / WAVES);
-            if (ina == 8)
-                hipLaunchKernelGGL((k_open_uniform_carry<8>), cgrid, dim3(BLOCK), WAVES * LINE_LDS_BYTES, s,
-                                   (const uint8_t *)in, in_stride, (uint8_t *)out, out_stride, nwaves, P, size,
-                                   (const uint8_t *)subkey, floor0, check, status, g_un0);
-            else
-                hipLaunchKernelGGL((k_open_uniform_carry<1>), cgrid, dim3(BLOCK), WAVES * LINE_LDS_BYTES, s,
-                                   (const uint8_t *)in, in_stride, (uint8_t *)out, out_stride, nwaves, P, size,
-                                   (const uint8_t *)subkey, floor0, check, status, g_un0);
+            hipLaunchKernelGGL((k_open_uniform_carry<8>), cgrid, dim3(BLOCK), WAVES * LINE_LDS_BYTES, s,
+                               (const uint8_t *)in, in_stride, (uint8_t *)out, out_stride, nwaves, P, size,
+                               (const uint8_t *)subkey, floor0, check, status, g_un0);
             const uint64_t done = blocks * 64ull * P;
             if (done < count) {
                 hipError_t e = hipGetLastError();
@@ -3550,14 +3701,9 @@ hipError_t czk_open_uniform(const void *in, uint64_t in_stride, void *out, uint6
                 const dim3 tgrid((rest + BLOCK - 1) / BLOCK);
                 const uint8_t *tin = (const uint8_t *)in + done * in_stride;
                 uint8_t *tout = (uint8_t *)out + done * out_stride;
-                if (ina == 8)
-                    hipLaunchKernelGGL((k_open_uniform<ST_LINES, true, 8>), tgrid, dim3(BLOCK), WAVES * LINE_LDS_BYTES,
-                                       s, tin, in_stride, tout, out_stride, rest, size, (const uint8_t *)subkey, floor0,
-                                       check, status + done, g_un0, 1);
-                else
-                    hipLaunchKernelGGL((k_open_uniform<ST_LINES, true, 1>), tgrid, dim3(BLOCK), WAVES * LINE_LDS_BYTES,
-                                       s, tin, in_stride, tout, out_stride, rest, size, (const uint8_t *)subkey, floor0,
-                                       check, status + done, g_un0, 1);
+                hipLaunchKernelGGL((k_open_uniform<ST_LINES, true, 8>), tgrid, dim3(BLOCK), WAVES * LINE_LDS_BYTES,
+                                   s, tin, in_stride, tout, out_stride, rest, size, (const uint8_t *)subkey, floor0,
+                                   check, status + done, g_un0, 1);
             }
             return hipGetLastError();
         }

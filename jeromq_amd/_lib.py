@@ -193,6 +193,11 @@ def lib():
         f = getattr(L, name)
         f.restype = res
         f.argtypes = args
+    # A/B and profiling runs only: CZ_TUNE="open_seg_carry=0,pair=1" sets cz_tune knobs at load
+    for kv in filter(None, os.environ.get("CZ_TUNE", "").split(",")):
+        k, v = kv.split("=")
+        if L.cz_tune(k.strip().encode(), int(v)) < 0:
+            raise CzError(f"CZ_TUNE: unknown knob {k!r}")
     _LIB = L
     return L
 

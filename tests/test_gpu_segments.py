@@ -402,3 +402,55 @@ def test_seal_segments_tiny_payloads_at_odd_offsets_end_of_buffer(torch_dev, sub
         lib.cz_tune(b"seal_ina", old)
     bad = np.nonzero(out != want)[0]
     assert bad.size == 0, f"{bad.size} bytes differ, first at {int(bad[0])}"
+
+
+def test_open_segments_8byte_packed_equal_lengths(torch_dev, subkeys, L):
+    """Open segments of 8-byte packed bodies in all 16 line phases: equal-length frames (full
+    waves of one chunk count on the line paths), long frames split into segments, and ragged ones,
+    sealed into 8-byte packed body slots (checked against the oracle), then opened from there with
+    tampered (early, middle and last block) and replayed frames mixed in; payloads equal the sealed
+    plaintext, rejected frames leave zeros."""
+    rng = np.random.default_rng(57)
+    lens = [167] * 2048 + [967] * 2048 + [4096] * 1024 + [8967] * 512 + [65536] * 64 + \
+        [int(x) for x in rng.integers(0, 3000, size=500)]
+    order = rng.permutation(len(lens))
+    lens = [lens[k] for k in order]
+    desc = np.zeros(len(lens), dtype=DESC_DTYPE)
+    io, oo = 0, 8
+    for i, n in enumerate(lens):
+        desc[i] = (io, oo, n, 0, 7 + 3 * i, i & 3, -1)
+        io += (n + 15) // 16 * 16
+        oo += (n + 33 + 7) // 8 * 8
+    assert (desc["out_off"] % 16 == 8).sum() > len(lens) // 3
+    hin = np.frombuffer(splitmix_bytes(io + 64, 61), dtype=np.uint8).copy()
+    ob = oo + 64
+    sealed, _ = _seal_seg(torch_dev, subkeys, desc, hin, ob, 64)
+    assert np.array_equal(sealed, _oracle_seal(desc, hin, ob))
+    odesc = np.zeros(len(lens), dtype=DESC_DTYPE)
+    po = 0
+    for i, n in enumerate(lens):
+        odesc[i] = (int(desc[i]["out_off"]), po, n + 33, 0, int(desc[i]["counter"]) - 1, 0x100, -1)
+        po += (n + 15) // 16 * 16
+    want = [L.CZ_STATUS_OK] * len(lens)
+    body = sealed.copy()
+    big = [i for i, n in enumerate(lens) if n >= 900]
+    for j, i in enumerate(rng.choice(big, size=60, replace=False)):
+        n = lens[i] + 33
+        where = [40, 64 + int(rng.integers(0, 64)), n // 2, n - 1][j % 4]
+        body[int(odesc[i]["in_off"]) + where] ^= 0x08
+        want[i] = L.CZ_STATUS_CRYPTO
+    for i in rng.choice(len(lens), size=20, replace=False):
+        if want[i] == L.CZ_STATUS_OK:
+            odesc[i]["counter"] += 1
+            want[i] = L.CZ_STATUS_SEQUENCE
+    st, pout, nn, plan = _open_seg(torch_dev, subkeys, odesc, body, po + 64, 64)
+    assert plan.ncomb > 0
+    assert list(st & 0xff) == want
+    for i, n in enumerate(lens):
+        o, oi = int(odesc[i]["out_off"]), int(desc[i]["in_off"])
+        if want[i] == L.CZ_STATUS_OK:
+            assert st[i] >> 8 == int(desc[i]["flags"]) & 0xff
+            assert pout[o:o + n].tobytes() == hin[oi:oi + n].tobytes(), f"frame {i} len {n}"
+        elif want[i] == L.CZ_STATUS_CRYPTO:
+            assert not pout[o:o + n].any(), f"frame {i} leaked plaintext"
+        assert nn[i] == int(desc[i]["counter"])

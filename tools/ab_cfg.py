@@ -3,6 +3,10 @@
 box-to-box clock differences cancel: every round times each workload back to back.
 
   python tools/ab_cfg.py --rounds 8 --steps 5 4k open4k "open4k --out-stride 4129"
+  python tools/ab_cfg.py zipf_open "zipf_open --tune open_seg_carry=0"
+
+A spec's `--tune key=value` (repeatable) sets that cz_tune knob around each of its steps and puts
+it back after, so one library's paths can be A/B'd against each other.
 
 Each spec is a bench.py config name plus optional bench layout flags.  Parity of every workload is
 spot-checked against the oracle first (bench.Workload.verify_sample).  Prints per-spec median /
@@ -31,10 +35,34 @@ def make(spec, frames, dev):
     ap.add_argument("--in-align", type=int, default=64)
     ap.add_argument("--out-align", type=int, default=128)
     ap.add_argument("--seg-blocks", type=int, default=128)
+    ap.add_argument("--tune", action="append", default=[])
     a = ap.parse_args(toks)
-    return bench.Workload(a.config, frames, 0, dev, out_align=a.out_align, seg_blocks=a.seg_blocks,
-                          in_align=a.in_align, plain_stride=a.plain_stride, in_stride=a.in_stride,
-                          out_stride=a.out_stride)
+    tune = [(k, int(v)) for k, v in (t.split("=") for t in a.tune)]
+    with tuned(tune):
+        wl = bench.Workload(a.config, frames, 0, dev, out_align=a.out_align, seg_blocks=a.seg_blocks,
+                            in_align=a.in_align, plain_stride=a.plain_stride, in_stride=a.in_stride,
+                            out_stride=a.out_stride)
+    wl.tune = tune
+    return wl
+
+
+class tuned:
+    def __init__(self, knobs):
+        self.knobs, self.old = knobs, []
+
+    def __enter__(self):
+        from jeromq_amd import _lib
+        for k, v in self.knobs:
+            old = _lib.lib().cz_tune(k.encode(), v)
+            if old < 0:
+                raise SystemExit(f"cz_tune: unknown knob {k}")
+            self.old.append((k, old))
+
+    def __exit__(self, *exc):
+        from jeromq_amd import _lib
+        for k, v in reversed(self.old):
+            _lib.lib().cz_tune(k.encode(), v)
+        self.old = []
 
 
 def main():
@@ -49,25 +77,28 @@ def main():
     wls = []
     for sp in a.specs:
         wl = make(sp, a.frames, dev)
-        wl.step()
-        wl.verify_sample()
+        with tuned(wl.tune):
+            wl.step()
+            wl.verify_sample()
         wls.append(wl)
     # ramp the clock out of idle
     for _ in range(20):
         for wl in wls:
-            wl.step()
+            with tuned(wl.tune):
+                wl.step()
     torch.cuda.synchronize()
     s = torch.cuda.current_stream()
     times = [[] for _ in wls]
     for _ in range(a.rounds):
         for k, wl in enumerate(wls):
-            wl.step()
-            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-            e0.record(s)
-            for _ in range(a.steps):
+            with tuned(wl.tune):
                 wl.step()
-            e1.record(s)
-            torch.cuda.synchronize()
+                e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+                e0.record(s)
+                for _ in range(a.steps):
+                    wl.step()
+                e1.record(s)
+                torch.cuda.synchronize()
             times[k].append(e0.elapsed_time(e1) / a.steps)
     base = None
     for sp, wl, t in zip(a.specs, wls, times):

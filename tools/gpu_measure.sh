@@ -31,20 +31,22 @@ run zipf_lane --config zipf_lane --no-cpu-baseline
 run zipf_open --config zipf_open --no-cpu-baseline
 run zipf_open_oa8 --config zipf_open --in-align 8 --out-align 8 --no-cpu-baseline
 run open4k_dense --config open4k --out-stride 4129 --no-cpu-baseline
+run open4k_dense8 --config open4k --out-stride 4136 --no-cpu-baseline
+run open4k_ps4224 --config open4k --plain-stride 4224 --no-cpu-baseline
 run 100b_packed --config 100b --in-stride 100 --no-cpu-baseline
 run 4k_in4097 --config 4k --in-stride 4097 --no-cpu-baseline
 for cfg in e2e4k engine beforenm nacl; do
   run $cfg --steps 10 --warmup 2 --config $cfg --no-cpu-baseline
 done
-for key in 4k zipf open4k 100b 4k_dense 4k_box zipf@ia8,oa8 zipf@oa1 zipf_open@ia8,oa8 open4k@os4129; do
+for key in 4k zipf open4k 100b 4k_dense 4k_box zipf@ia8,oa8 zipf@oa1 zipf_open@ia8,oa8 open4k@os4129 open4k@os4136; do
   args=$(python3 tools/pmc_key.py args "$key"); f=$(python3 tools/pmc_key.py file "$key")
   echo "== rocprofv3 kernel trace $key"
   timeout -k 10 300 rocprofv3 --kernel-trace --stats -T --output-format csv -d gpurun_out/prof_$f -o run -- python3 bench.py --steps 10 --warmup 2 --no-cpu-baseline --no-roundtrip $args > gpurun_out/prof_$f.log 2>&1 || { tail gpurun_out/prof_$f.log; exit 6; }
 done
 fi
 if [ "${PART:-bench}" = pmc ]; then
-bash tools/gpu_traffic.sh 4k 100b zipf open4k 4k_dense 4k_box zipf@oa1 zipf_open@ia8,oa8 open4k@os4129 || exit 7
-bash tools/gpu_valu.sh 4k 100b zipf open4k 4k_dense 4k_box zipf@ia8,oa8 zipf@oa1 zipf_open@ia8,oa8 open4k@os4129 || exit 8
+bash tools/gpu_traffic.sh 4k 100b zipf open4k 4k_dense 4k_box zipf@oa1 zipf_open@ia8,oa8 open4k@os4129 open4k@os4136 || exit 7
+bash tools/gpu_valu.sh 4k 100b zipf open4k 4k_dense 4k_box zipf@ia8,oa8 zipf@oa1 zipf_open@ia8,oa8 open4k@os4129 open4k@os4136 || exit 8
 bash tools/gpu_stall.sh 4k open4k zipf > gpurun_out/stall_measure.log 2>&1 || { tail gpurun_out/stall_measure.log; exit 9; }
 cp profiles/pmc_traffic.json gpurun_out/pmc_traffic_measure.json
 fi

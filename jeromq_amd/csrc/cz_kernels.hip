@@ -115,6 +115,16 @@ __device__ __forceinline__ V4 zero4() { return V4{0u, 0u, 0u, 0u}; }
 // Byte-granular pieces of a 16-byte unit.  gfx950 executes unaligned global and LDS
 // accesses (the compiler emits them for align-1 types), so a clipped edge unit leaves in at
 // most 4 stores (8, 4, 2, 1 bytes) instead of a byte loop.
+// EmitShiftLines' chunk writes at byte offsets: 0 = dword funnel (alignbyte + 17 ds_write_b32),
+// 1 = ds_write_b128 at the byte address for outputs off 8-byte alignment, 2 = also for 8-byte ones
+#ifndef CZ_ULDS
+#define CZ_ULDS 1
+#endif
+// inputs at any byte offset: 1 = 16-byte global loads at the byte address (the hardware's
+// unaligned access) instead of dword-aligned loads and a byte funnel
+#ifndef CZ_UGLD
+#define CZ_UGLD 0
+#endif
 typedef uint64_t u64_ua __attribute__((aligned(1)));
 typedef uint32_t u32_ua __attribute__((aligned(1)));
 typedef uint16_t u16_ua __attribute__((aligned(1)));
@@ -1163,6 +1173,9 @@ __device__ __forceinline__ u32 open_frame(const uint8_t *__restrict__ in, u32 si
     auto LF = [&](u32 off) -> V4 {
         if constexpr (INA == 16) {
             return ld16f<AL>(in + off);
+        } else if constexpr (INA == 1 && CZ_UGLD) {
+            const v4u_t r = *reinterpret_cast<const v4u_ua *>(in + off);  // global_load_dwordx4 at the byte address
+            return V4{r.x, r.y, r.z, r.w};
         } else {
             const uint4 r = *reinterpret_cast<const u4_a4 *>(in4 + off);
             if constexpr (INA == 8)
@@ -1419,7 +1432,7 @@ __device__ __forceinline__ u32 open_frame(const uint8_t *__restrict__ in, u32 si
             }
             for (u32 k = 1; !CARRY && 2u * k + 1u < nfull; k++) {
                 u32 M[32];
-                if constexpr (INA == 1) {
+                if constexpr (INA == 1 && !CZ_UGLD) {
                     // 8 loads from the dword-aligned line below and the dword after it, funnelled
                     // inside open_block (after the keystream)
                     const uint8_t *src4 = in4 + 128u * k;
@@ -1813,6 +1826,25 @@ struct EmitShiftLinesT {
         // the next chunk's E[0] rewrites that dword whole.
         // A wave whose offsets are all 16- or 8-byte multiples writes the chunk as it is, with
         // ds_write_b128 / b64 at aligned addresses (no funnel); only the other waves pay it.
+#if CZ_ULDS
+        // ds_write_b128 at any byte address (ROCm runs LDS in unaligned mode; the hardware splits
+        // the access): the chunk's bytes land exactly at [pos, pos + 64), no funnel, no tail dword
+        const u32 b = 0u;
+        uint8_t *row0 = rows + lane * SROW + SHEAD;
+        if (walign == 16u) {
+#pragma unroll
+            for (u32 c = 0; c < 4; c++)
+                reinterpret_cast<uint4 *>(row0 + pos)[c] = make_uint4(D[4 * c], D[4 * c + 1], D[4 * c + 2], D[4 * c + 3]);
+        } else if (CZ_ULDS == 1 && walign == 8u) {
+#pragma unroll
+            for (u32 c = 0; c < 8; c++)
+                reinterpret_cast<uint2 *>(row0 + pos)[c] = make_uint2(D[2 * c], D[2 * c + 1]);
+        } else {
+#pragma unroll
+            for (u32 c = 0; c < 4; c++)
+                *reinterpret_cast<v4u_ua *>(row0 + pos + 16u * c) = v4u_t{D[4 * c], D[4 * c + 1], D[4 * c + 2], D[4 * c + 3]};
+        }
+#else
         const u32 b = (4u - (pos & 3u)) & 3u;
         uint8_t *row0 = rows + lane * SROW + SHEAD;
         if (walign == 16u) {
@@ -1832,6 +1864,7 @@ struct EmitShiftLinesT {
             w[16] = funnel(0u, D[15], b);
             carry_w = D[15];
         }
+#endif
         const bool done = (t & 64u) != 0u;
         if (mixed) {
             flush<FL_MIXED>(q);
@@ -2289,7 +2322,10 @@ __device__ __forceinline__ u32 open_segment(const uint8_t *__restrict__ in, u32 
     const u32 ina = ANY ? (u32)(uintptr_t)in & 3u : 0u;
     const uint8_t *in4 = in - ina;
     auto ldf = [&](const uint8_t *p) -> V4 {  // all 16 bytes inside the body
-        if constexpr (ANY) {
+        if constexpr (ANY && CZ_UGLD) {
+            const v4u_t r = *reinterpret_cast<const v4u_ua *>(p);
+            return V4{r.x, r.y, r.z, r.w};
+        } else if constexpr (ANY) {
             const uint8_t *q = in4 + (p - in);
             const uint4 r = *reinterpret_cast<const u4_a4 *>(q);
             const u32 r4 = ina ? *reinterpret_cast<const u32 *>(q + 16) : 0u;

@@ -1808,6 +1808,9 @@ struct EmitShiftLinesT {
     // for the next line (LDS ops of one wave execute in order: the flush's reads come first)
     __device__ __forceinline__ void shift_row(u32 end)
     {
+#ifdef CZ_DIAG_NOSHIFTROW  // timing diagnostic only: wrong output
+        return;
+#endif
         asm volatile("" ::: "memory");
         uint4 *row = reinterpret_cast<uint4 *>(rows + lane * SROW + SHEAD);
 #pragma unroll

@@ -879,6 +879,9 @@ __device__ __forceinline__ void seal_frame(const uint8_t *__restrict__ in0, u32 
                 // behind it, so a line is read in pieces and L2 re-fetches it: FETCH 1.20x the box
                 // bytes.  A sched_barrier here keeps the 8 loads together and the first wait ~1570
                 // instructions later -- and measured 14% SLOWER (interleaved A/B).)
+#ifdef CZ_BOX_FENCE
+                __builtin_amdgcn_sched_barrier(0);
+#endif
                 box_full_block(2u * k, L);
                 box_full_block(2u * k + 1u, L + 16);
                 blk = 2u * k + 2u;

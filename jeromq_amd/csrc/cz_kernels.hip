@@ -145,6 +145,15 @@ typedef v4u_t v4u_ua __attribute__((aligned(1)));
 typedef uint4 u4_a4 __attribute__((aligned(4)));  // a 16-byte load from a dword-aligned address
 typedef __attribute__((address_space(1))) v4u_ua g_v4u_ua;
 
+// Cache policy of the line stores (gfx940 encoding: 1 sc0, 2 nt, 16 sc1).  Seal emitters store
+// non-temporal: interleaved A/B, Zipf seal +1.4%, dense seal +1.9%, headline +0.3%; the open's
+// 4 KiB plaintext slots lose 1.4% with it and keep the default.
+#ifndef CZ_SEAL_STORE_CPOL
+#define CZ_SEAL_STORE_CPOL 2
+#endif
+#ifndef CZ_OPEN_STORE_CPOL
+#define CZ_OPEN_STORE_CPOL 0
+#endif
 // 16-byte line store through a buffer resource: `base` wave-uniform (SGPRs), `voff` this lane's
 // 32-bit offset, soffset the constant 0.  Never give these stores a REGISTER soffset: LLVM's
 // hazard recognizer assumes a MUBUF store with a register soffset has no store-data hazard and
@@ -152,11 +161,12 @@ typedef __attribute__((address_space(1))) v4u_ua g_v4u_ua;
 // writes the new value (round 3: one dword per 16 bytes replaced by an LDS address, a few lines
 // per 2^20-frame Zipf batch).  With soffset 0 it inserts the wait state, and
 // tests/test_isa_hazards.py checks the listing for any MUBUF store with a register soffset.
+template <int CP = CZ_OPEN_STORE_CPOL>
 __device__ __forceinline__ void buf_store16(u64 base, u32 voff, uint4 v)
 {
     const __amdgpu_buffer_rsrc_t rs =
         __builtin_amdgcn_make_buffer_rsrc(reinterpret_cast<void *>((uintptr_t)base), 0, (int)0xffffffffu, 0x00020000);
-    __builtin_amdgcn_raw_buffer_store_b128(v4u_t{v.x, v.y, v.z, v.w}, rs, (int)voff, 0, 0);
+    __builtin_amdgcn_raw_buffer_store_b128(v4u_t{v.x, v.y, v.z, v.w}, rs, (int)voff, 0, CP);
 }
 
 // wave-uniform copy of a 64-bit value (each half through u32: readfirstlane returns int, and a low
@@ -381,7 +391,8 @@ struct EmitDirect {
 // Whole-line staging for a full wave of equal-length frames whose slots are
 // 128-byte multiples (stride % 128 == 0, base 16-byte aligned).  Each frame
 // owns its slot: bytes of the last line beyond `total` are written as zero.
-struct EmitLines {
+template <int CP>
+struct EmitLinesT {
     static constexpr bool cooperative = true;  // every lane of the wave must run the same chunk sequence
     uint4 *lds;        // this wave's 64 x 8 chunks
     uint8_t *wbase;    // slot of frame 0 of this wave
@@ -436,7 +447,7 @@ struct EmitLines {
             }
             p += step;
 #else
-                buf_store16(lb + (u64)(j * step), voff, v);
+                buf_store16<CP>(lb + (u64)(j * step), voff, v);
 #endif
         }
     }
@@ -536,6 +547,8 @@ struct EmitLines {
             *reinterpret_cast<uint4 *>(mine + o) = make_uint4(0u, 0u, 0u, 0u);
     }
 };
+using EmitLines = EmitLinesT<CZ_OPEN_STORE_CPOL>;
+using EmitLinesSeal = EmitLinesT<CZ_SEAL_STORE_CPOL>;
 
 #ifdef CZ_FLUSH2
 // A/B build only (-DCZ_FLUSH2, DESIGN.md section 6, "the write-path clock"): EmitLines for the
@@ -1668,7 +1681,7 @@ struct WaveRel {
     }
 };
 
-template <bool UNI>
+template <bool UNI, int CP = CZ_OPEN_STORE_CPOL>
 struct EmitShiftLinesT {
     static constexpr bool cooperative = true;
     uint8_t *rows;   // this wave's 64 rows of SROW bytes
@@ -1739,7 +1752,7 @@ struct EmitShiftLinesT {
                     for (u32 j = 0; j < 8; j++) {
                         const u32 F = 8u * j + r;
                         const uint4 v = *reinterpret_cast<const uint4 *>(rows + F * SROW + SHEAD + 16u * c);
-                        buf_store16(lb, loff[j], v);
+                        buf_store16<CP>(lb, loff[j], v);
                     }
                     return;
                 }
@@ -1753,7 +1766,7 @@ struct EmitShiftLinesT {
                     const u32 F = 8u * j + r;
                     const uint4 v = *reinterpret_cast<const uint4 *>(rows + F * SROW + SHEAD + 16u * c);
                     const u32 lo = (u32)__builtin_amdgcn_ds_bpermute((int)(F << 2), (int)wr.rel);
-                    buf_store16(lb, (lo & ~127u) | (16u * c), v);
+                    buf_store16<CP>(lb, (lo & ~127u) | (16u * c), v);
                 }
                 return;
             }
@@ -1911,6 +1924,8 @@ struct EmitShiftLinesT {
 };
 using EmitShiftLines = EmitShiftLinesT<false>;
 using EmitShiftLinesUni = EmitShiftLinesT<true>;
+using EmitShiftLinesSeal = EmitShiftLinesT<false, CZ_SEAL_STORE_CPOL>;
+using EmitShiftLinesUniSeal = EmitShiftLinesT<true, CZ_SEAL_STORE_CPOL>;
 
 // Line staging for a wave of segments at arbitrary 16-byte aligned bases.  Like
 // EmitLines, 8 lanes write one 128-byte output line per store instruction, but
@@ -1920,7 +1935,8 @@ using EmitShiftLinesUni = EmitShiftLinesT<true>;
 // is padding).  emit/finish/close must be reached by all 64 lanes together:
 // ds_bpermute from an inactive lane returns garbage, not its base.
 constexpr u32 SEG_LDS_BYTES = LINE_LDS_BYTES;  // EmitSegLines: 64 x 128-byte line buffer per wave
-struct EmitSegLines {
+template <int CP>
+struct EmitSegLinesT {
     static constexpr bool cooperative = true;
     uint4 *lds;      // this wave's 64 x 8 chunks
     uint8_t *mine;
@@ -1951,7 +1967,7 @@ struct EmitSegLines {
             for (u32 j = 0; j < 8; j++) {
                 const u32 F = 8u * j + r;
                 const uint4 v = lds[F * 8u + (c ^ (F & 7u))];
-                buf_store16(lb, (u32)__builtin_amdgcn_ds_bpermute((int)(F << 2), (int)wr.rel) + 16u * c, v);
+                buf_store16<CP>(lb, (u32)__builtin_amdgcn_ds_bpermute((int)(F << 2), (int)wr.rel) + 16u * c, v);
             }
             return;
         }
@@ -2012,6 +2028,8 @@ struct EmitSegLines {
         }
     }
 };
+using EmitSegLines = EmitSegLinesT<CZ_OPEN_STORE_CPOL>;
+using EmitSegLinesSeal = EmitSegLinesT<CZ_SEAL_STORE_CPOL>;
 
 // Reorder the work items of one full workgroup so that each wave holds outputs of one
 // EmitShiftLines class (bit 6 of the output address): such a wave flushes once per chunk pair
@@ -2530,7 +2548,7 @@ __device__ __forceinline__ void seal_uniform_body(const uint8_t *__restrict__ in
 #ifdef CZ_FLUSH2
             using EmL = EmitLines2;
 #else
-            using EmL = EmitLines;
+            using EmL = EmitLinesSeal;
 #endif
             EmL em{smem + (threadIdx.x >> 6) * (LINE_LDS_BYTES / 16), out + (uint64_t)wave_first * out_stride,
                    dst, out_stride, lane, mlen, 0u, true,
@@ -2541,14 +2559,14 @@ __device__ __forceinline__ void seal_uniform_body(const uint8_t *__restrict__ in
                 seal_frame<MODE, true, EmL, PAIR, false, true, INA>(src, len, fl, counter0 + i, key, em);
         } else if constexpr (ST == ST_SHIFT) {
             // bodies at any byte offset (dense packing, wire layout): byte-shifted line staging
-            EmitShiftLinesUni em{reinterpret_cast<uint8_t *>(smem) + (threadIdx.x >> 6) * SHIFT_LDS_BYTES, dst, lane,
+            EmitShiftLinesUniSeal em{reinterpret_cast<uint8_t *>(smem) + (threadIdx.x >> 6) * SHIFT_LDS_BYTES, dst, lane,
                                  mlen, 0u, 0u};
             em.init(true);
             em.init_uniform(i - blockIdx.x * BLOCK, (u32)out_stride, out + (uint64_t)blockIdx.x * BLOCK * out_stride);
             if (un0)
-                seal_frame<MODE, true, EmitShiftLinesUni, PAIR, true, true, INA>(src, len, fl, counter0 + i, key, em);
+                seal_frame<MODE, true, EmitShiftLinesUniSeal, PAIR, true, true, INA>(src, len, fl, counter0 + i, key, em);
             else
-                seal_frame<MODE, true, EmitShiftLinesUni, PAIR, false, true, INA>(src, len, fl, counter0 + i, key, em);
+                seal_frame<MODE, true, EmitShiftLinesUniSeal, PAIR, false, true, INA>(src, len, fl, counter0 + i, key, em);
         } else {
             const u32 st = (u32)out_stride;
             EmitRegion em{smem + (threadIdx.x >> 6) * ((64u * st) >> 4), out + (uint64_t)wave_first * out_stride, st,
@@ -2911,18 +2929,18 @@ __device__ __forceinline__ void seal_segments_body(const cz_frame_desc *__restri
                 const bool line_al = (((uintptr_t)dst) & 127u) == 0;
                 if (__builtin_amdgcn_ballot_w64(!al) == 0 &&
                     (!(mode & SEGMODE_SHIFT16) || __builtin_amdgcn_ballot_w64(!line_al) == 0)) {
-                    EmitSegLines em{reinterpret_cast<uint4 *>(wl), dst, lane, total, 0u, 0u};
+                    EmitSegLinesSeal em{reinterpret_cast<uint4 *>(wl), dst, lane, total, 0u, 0u};
                     em.init(sg.first_block == 0);
-                    seal_segment<true, EmitSegLines, true>(src, d.len, d.flags & 0xffu, d.counter, key,
+                    seal_segment<true, EmitSegLinesSeal, true>(src, d.len, d.flags & 0xffu, d.counter, key,
                                                            sg.first_block, b1, rec, em, wave_max(nch));
                 } else {
-                    EmitShiftLines em{wl, dst, lane, total, 0u, 0u};
+                    EmitShiftLinesSeal em{wl, dst, lane, total, 0u, 0u};
                     em.init(sg.first_block == 0);
-                    seal_segment<true, EmitShiftLines, true>(src, d.len, d.flags & 0xffu, d.counter, key,
+                    seal_segment<true, EmitShiftLinesSeal, true>(src, d.len, d.flags & 0xffu, d.counter, key,
                                                              sg.first_block, b1, rec, em, wave_max(nch));
                 }
             } else {
-                EmitSegLines em{reinterpret_cast<uint4 *>(wl), dst, lane, total, 0u, 0u};
+                EmitSegLinesSeal em{reinterpret_cast<uint4 *>(wl), dst, lane, total, 0u, 0u};
                 em.init(sg.first_block == 0);
                 seal_segment<true>(src, d.len, d.flags & 0xffu, d.counter, key, sg.first_block, b1, rec, em);
             }
@@ -2935,13 +2953,13 @@ __device__ __forceinline__ void seal_segments_body(const cz_frame_desc *__restri
         if (allow_lines && pair && full_wave && (mode & SEGMODE_ANYIN)) {
             const u32 lane = threadIdx.x & 63u;
             uint8_t *wl = reinterpret_cast<uint8_t *>(smem) + (threadIdx.x >> 6) * SHIFT_LDS_BYTES;
-            EmitShiftLines em{wl, dst, lane, total, 0u, 0u};
+            EmitShiftLinesSeal em{wl, dst, lane, total, 0u, 0u};
             em.init(sg.first_block == 0);
             if (__builtin_amdgcn_ballot_w64((((uintptr_t)src) & 7u) != 0u) == 0)
-                seal_segment<true, EmitShiftLines, true, 8>(src, d.len, d.flags & 0xffu, d.counter, key,
+                seal_segment<true, EmitShiftLinesSeal, true, 8>(src, d.len, d.flags & 0xffu, d.counter, key,
                                                             sg.first_block, b1, rec, em, wave_max(nch));
             else
-                seal_segment<true, EmitShiftLines, true, 1>(src, d.len, d.flags & 0xffu, d.counter, key,
+                seal_segment<true, EmitShiftLinesSeal, true, 1>(src, d.len, d.flags & 0xffu, d.counter, key,
                                                             sg.first_block, b1, rec, em, wave_max(nch));
             return;
         }

@@ -154,6 +154,12 @@ typedef __attribute__((address_space(1))) v4u_ua g_v4u_ua;
 #ifndef CZ_OPEN_STORE_CPOL
 #define CZ_OPEN_STORE_CPOL 0
 #endif
+// opens of bodies off 16-byte alignment, of plaintext at any byte offset, and of segments: nt
+// (dense open +2.2%, Zipf open +1.5% / +2.1% at the 8-byte table; the aligned open into 4 KiB
+// plaintext slots and the carried-line open keep the default: -0.7..-1.4% / +-0 with nt)
+#ifndef CZ_OPEN_ANY_STORE_CPOL
+#define CZ_OPEN_ANY_STORE_CPOL 2
+#endif
 // 16-byte line store through a buffer resource: `base` wave-uniform (SGPRs), `voff` this lane's
 // 32-bit offset, soffset the constant 0.  Never give these stores a REGISTER soffset: LLVM's
 // hazard recognizer assumes a MUBUF store with a register soffset has no store-data hazard and
@@ -276,6 +282,21 @@ __device__ __forceinline__ V4 ld16f(const uint8_t *__restrict__ p)
 // 8-byte aligned input (the open of bodies packed at 8-byte offsets): a
 // 16-byte chunk as two naturally aligned 8-byte loads.  ld16_8 reads the second half only when the
 // object reaches into it (an aligned 8-byte piece holding a valid byte cannot cross a page).
+// the seal's payload loads: non-temporal with CZ_SEAL_LOAD_NT (A/B), ld16f otherwise
+#ifndef CZ_SEAL_LOAD_NT
+#define CZ_SEAL_LOAD_NT 0
+#endif
+template <bool AL>
+__device__ __forceinline__ V4 ld16f_in(const uint8_t *__restrict__ p)
+{
+#if CZ_SEAL_LOAD_NT
+    if constexpr (AL) {
+        const v4u_t v = __builtin_nontemporal_load(reinterpret_cast<const v4u_t *>(p));
+        return V4{v.x, v.y, v.z, v.w};
+    }
+#endif
+    return ld16f<AL>(p);
+}
 __device__ __forceinline__ V4 ld16f_8(const uint8_t *__restrict__ p)
 {
 #ifdef CZ_AL8_X4
@@ -774,7 +795,7 @@ __device__ __forceinline__ void seal_frame(const uint8_t *__restrict__ in0, u32 
     }
     auto ldF = [&](const uint8_t *p) -> V4 {  // all 16 bytes inside the payload
         if constexpr (INA == 16) {
-            return ld16f<AL>(p);
+            return ld16f_in<AL>(p);
         } else {
             const uint4 r = *reinterpret_cast<const u4_a4 *>(p);
             return V4{r.x, r.y, r.z, r.w};
@@ -885,7 +906,7 @@ __device__ __forceinline__ void seal_frame(const uint8_t *__restrict__ in0, u32 
                 const uint8_t *src = in + 128u * k;
 #pragma unroll
                 for (int c = 0; c < 8; c++) {
-                    V4 v = ld16f<AL>(src + 16 * c);
+                    V4 v = ld16f_in<AL>(src + 16 * c);
                     L[4 * c] = v.x; L[4 * c + 1] = v.y; L[4 * c + 2] = v.z; L[4 * c + 3] = v.w;
                 }
                 // (The scheduler sinks each of these loads to just before its first use, with a vmcnt(0)
@@ -956,7 +977,7 @@ __device__ __forceinline__ void seal_frame(const uint8_t *__restrict__ in0, u32 
 #pragma unroll
                 for (int c = 6; c < 8; c++) {
                     if (inlen > o + 16u * c) {
-                        V4 v = INA == 16 ? ld16f<AL>(src + 16 * c) : ldP(src + 16 * c, inlen - o - 16u * c);
+                        V4 v = INA == 16 ? ld16f_in<AL>(src + 16 * c) : ldP(src + 16 * c, inlen - o - 16u * c);
                         L[4 * c] = v.x; L[4 * c + 1] = v.y; L[4 * c + 2] = v.z; L[4 * c + 3] = v.w;
                     }
                 }
@@ -1043,10 +1064,10 @@ __device__ __forceinline__ void seal_frame(const uint8_t *__restrict__ in0, u32 
             carry = q3.w;
         } else {
             const uint8_t *src = in + 64u * blk;
-            q0 = ld16f<AL>(src);
-            q1 = ld16f<AL>(src + 16);
-            q2 = ld16f<AL>(src + 32);
-            q3 = ld16f<AL>(src + 48);
+            q0 = ld16f_in<AL>(src);
+            q1 = ld16f_in<AL>(src + 16);
+            q2 = ld16f_in<AL>(src + 32);
+            q3 = ld16f_in<AL>(src + 48);
             ksblock(x, blk, 0u);
             u32 W[16] = {q0.x, q0.y, q0.z, q0.w, q1.x, q1.y, q1.z, q1.w,
                          q2.x, q2.y, q2.z, q2.w, q3.x, q3.y, q3.z, q3.w};
@@ -2099,7 +2120,7 @@ __device__ __forceinline__ void seal_segment(const uint8_t *__restrict__ in0, u3
     }
     auto ldF = [&](const uint8_t *p) -> V4 {
         if constexpr (INA == 16) {
-            return ld16f<AL>(p);
+            return ld16f_in<AL>(p);
         } else {
             const uint4 r = *reinterpret_cast<const u4_a4 *>(p);
             return V4{r.x, r.y, r.z, r.w};
@@ -2732,25 +2753,27 @@ __global__ __launch_bounds__(BLOCK) CZ_OCC CZ_OPEN_UNI_OCC void k_open_uniform(c
         const u32 lane = threadIdx.x & 63u;
         const bool un0 = allow_un0 && wave_uniform(INA >= 8 ? *reinterpret_cast<const u32 *>(src + 8) : ld32<false>(src + 8));
         if constexpr (ST == ST_LINES) {
-            EmitLines em{smem + (threadIdx.x >> 6) * (LINE_LDS_BYTES / 16), out + (uint64_t)wave_first * out_stride,
-                         dst, out_stride, lane, nout, 0u, false};
+            // bodies off 16-byte alignment (the dense wire layout) store non-temporal
+            using EmL = EmitLinesT<INA == 16 ? CZ_OPEN_STORE_CPOL : CZ_OPEN_ANY_STORE_CPOL>;
+            EmL em{smem + (threadIdx.x >> 6) * (LINE_LDS_BYTES / 16), out + (uint64_t)wave_first * out_stride,
+                   dst, out_stride, lane, nout, 0u, false};
             if (un0)
-                st = open_frame<MODE_ZMQ, true, EmitLines, PAIR, true, true, INA>(src, size, key, check != 0, floor, &fl,
-                                                                                 &nonce, 0, em);
+                st = open_frame<MODE_ZMQ, true, EmL, PAIR, true, true, INA>(src, size, key, check != 0, floor, &fl,
+                                                                           &nonce, 0, em);
             else
-                st = open_frame<MODE_ZMQ, true, EmitLines, PAIR, false, true, INA>(src, size, key, check != 0, floor, &fl,
-                                                                                  &nonce, 0, em);
+                st = open_frame<MODE_ZMQ, true, EmL, PAIR, false, true, INA>(src, size, key, check != 0, floor, &fl,
+                                                                            &nonce, 0, em);
         } else if constexpr (ST == ST_SHIFT) {
-            EmitShiftLinesUni em{reinterpret_cast<uint8_t *>(smem) + (threadIdx.x >> 6) * SHIFT_LDS_BYTES, dst, lane,
-                                 nout, 0u, 0u};
+            using EmS = EmitShiftLinesT<true, CZ_OPEN_ANY_STORE_CPOL>;  // plaintext at any byte offset
+            EmS em{reinterpret_cast<uint8_t *>(smem) + (threadIdx.x >> 6) * SHIFT_LDS_BYTES, dst, lane, nout, 0u, 0u};
             em.init(false);
             em.init_uniform(i - blockIdx.x * BLOCK, (u32)out_stride, out + (uint64_t)blockIdx.x * BLOCK * out_stride);
             if (un0)
-                st = open_frame<MODE_ZMQ, true, EmitShiftLinesUni, PAIR, true, true, INA>(src, size, key, check != 0,
-                                                                                         floor, &fl, &nonce, 0, em);
+                st = open_frame<MODE_ZMQ, true, EmS, PAIR, true, true, INA>(src, size, key, check != 0, floor, &fl,
+                                                                           &nonce, 0, em);
             else
-                st = open_frame<MODE_ZMQ, true, EmitShiftLinesUni, PAIR, false, true, INA>(src, size, key, check != 0,
-                                                                                          floor, &fl, &nonce, 0, em);
+                st = open_frame<MODE_ZMQ, true, EmS, PAIR, false, true, INA>(src, size, key, check != 0, floor, &fl,
+                                                                            &nonce, 0, em);
         } else {
             const u32 ost = (u32)out_stride;
             EmitRegion em{smem + (threadIdx.x >> 6) * ((64u * ost) >> 4), out + (uint64_t)wave_first * out_stride,
@@ -3082,19 +3105,19 @@ __global__ __launch_bounds__(BLOCK) CZ_OPEN_SEG_OCC void k_open_segments(const c
         const bool line_al = (((uintptr_t)dst) & 127u) == 0;  // as in seal_segments_body
         if (__builtin_amdgcn_ballot_w64(!al) == 0 &&
             (!(mode & SEGMODE_SHIFT16) || __builtin_amdgcn_ballot_w64(!line_al) == 0)) {
-            EmitSegLines em{reinterpret_cast<uint4 *>(wl), dst, lane, total, 0u, 0u};
+            EmitSegLinesT<CZ_OPEN_ANY_STORE_CPOL> em{reinterpret_cast<uint4 *>(wl), dst, lane, total, 0u, 0u};
             em.init(false);
             st = open_segment<true>(src, d.len, key, n0, n1, sg.first_block, b1, rec, fl, em);
         } else {  // plaintext at any byte offset
-            EmitShiftLines em{wl, dst, lane, total, 0u, 0u};
+            using EmS = EmitShiftLinesT<false, CZ_OPEN_ANY_STORE_CPOL>;
+            EmS em{wl, dst, lane, total, 0u, 0u};
             em.init(false);
             if (__builtin_amdgcn_ballot_w64(!in_al) == 0)
                 st = open_segment<true>(src, d.len, key, n0, n1, sg.first_block, b1, rec, fl, em);
             else if (__builtin_amdgcn_ballot_w64(!in_al8) == 0)
-                st = open_segment<false, EmitShiftLines, true>(src, d.len, key, n0, n1, sg.first_block, b1, rec, fl, em);
+                st = open_segment<false, EmS, true>(src, d.len, key, n0, n1, sg.first_block, b1, rec, fl, em);
             else
-                st = open_segment<false, EmitShiftLines, false, true>(src, d.len, key, n0, n1, sg.first_block, b1, rec,
-                                                                      fl, em);
+                st = open_segment<false, EmS, false, true>(src, d.len, key, n0, n1, sg.first_block, b1, rec, fl, em);
         }
         if (!rec)
             status[sg.frame] = (uint16_t)(st | (st == CZ_STATUS_OK ? (fl << 8) : 0u));

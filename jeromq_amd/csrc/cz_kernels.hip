@@ -705,7 +705,8 @@ struct EmitLines2 {
 // 64 slots (64 * stride <= REGION_MAX, stride % 16 == 0) are assembled in LDS
 // and written with contiguous 1 KiB store instructions.  Slot bytes beyond
 // `total` are written as zero.
-struct EmitRegion {
+template <int CP>
+struct EmitRegionT {
     static constexpr bool cooperative = true;
     uint4 *lds;        // 64 * stride bytes
     uint8_t *wbase;
@@ -741,8 +742,13 @@ struct EmitRegion {
             lds[(lane * stride + o) >> 4] = make_uint4(0u, 0u, 0u, 0u);
         const u32 n16 = (64u * stride) >> 4;
         asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // the other lanes' ds_writes of the region
-        for (u32 k = lane; k < n16; k += 64u)
-            reinterpret_cast<uint4 *>(wbase)[k] = lds[k];
+        for (u32 k = lane; k < n16; k += 64u) {
+            const uint4 v = lds[k];
+            if constexpr (CP == 2)
+                __builtin_nontemporal_store(v4u_t{v.x, v.y, v.z, v.w}, reinterpret_cast<v4u_t *>(wbase) + k);
+            else
+                reinterpret_cast<uint4 *>(wbase)[k] = v;
+        }
     }
     // zero a rejected frame's slot in LDS (per lane), then the converged region store
     __device__ __forceinline__ void close(bool bad)
@@ -757,6 +763,8 @@ struct EmitRegion {
             lds[(lane * stride + o) >> 4] = make_uint4(0u, 0u, 0u, 0u);
     }
 };
+using EmitRegion = EmitRegionT<CZ_OPEN_STORE_CPOL>;
+using EmitRegionSeal = EmitRegionT<CZ_SEAL_STORE_CPOL == 2 ? 2 : 0>;
 
 // --------------------------------------------------------------------------
 // SEAL one frame.
@@ -2590,12 +2598,12 @@ __device__ __forceinline__ void seal_uniform_body(const uint8_t *__restrict__ in
                 seal_frame<MODE, true, EmitShiftLinesUniSeal, PAIR, false, true, INA>(src, len, fl, counter0 + i, key, em);
         } else {
             const u32 st = (u32)out_stride;
-            EmitRegion em{smem + (threadIdx.x >> 6) * ((64u * st) >> 4), out + (uint64_t)wave_first * out_stride, st,
+            EmitRegionSeal em{smem + (threadIdx.x >> 6) * ((64u * st) >> 4), out + (uint64_t)wave_first * out_stride, st,
                           lane, mlen};
             if (un0)
-                seal_frame<MODE, true, EmitRegion, PAIR, true, true, INA>(src, len, fl, counter0 + i, key, em);
+                seal_frame<MODE, true, EmitRegionSeal, PAIR, true, true, INA>(src, len, fl, counter0 + i, key, em);
             else
-                seal_frame<MODE, true, EmitRegion, PAIR, false, true, INA>(src, len, fl, counter0 + i, key, em);
+                seal_frame<MODE, true, EmitRegionSeal, PAIR, false, true, INA>(src, len, fl, counter0 + i, key, em);
         }
         return;
     }

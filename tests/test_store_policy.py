@@ -13,6 +13,7 @@ import pytest
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, ROOT)
+REGION = "_ZN12_GLOBAL__N_114k_seal_uniformILi2ELb0ELi0E"  # 100 B seal: EmitRegion's whole-region stores
 
 
 @pytest.fixture(scope="module")
@@ -36,7 +37,8 @@ def line_stores():
                 out.setdefault(cur, [])
                 continue
             t = ln.split("//")[0].strip()
-            if cur and t.startswith("buffer_store_dwordx4"):
+            if cur and (t.startswith("buffer_store_dwordx4") or
+                        (cur.startswith(REGION) and t.startswith("global_store_dwordx4"))):
                 out[cur].append(" nt" in f" {t} ")
     return out
 
@@ -67,3 +69,9 @@ def test_nontemporal_line_stores(line_stores, prefix):
 def test_default_policy_line_stores(line_stores, prefix):
     st = _kernel(line_stores, prefix)
     assert st and not any(st), f"{prefix}: {sum(st)} of {len(st)} line stores nt"
+
+
+def test_region_seal_stores_nontemporal(line_stores):
+    """The 100 B seal's region stores (global_store_dwordx4 of the staged 64-slot region) are nt."""
+    st = _kernel(line_stores, REGION)
+    assert st and any(st), "no nt region store in the 100 B seal"

@@ -172,6 +172,9 @@ __device__ __forceinline__ void buf_store16(u64 base, u32 voff, uint4 v)
 {
     const __amdgpu_buffer_rsrc_t rs =
         __builtin_amdgcn_make_buffer_rsrc(reinterpret_cast<void *>((uintptr_t)base), 0, (int)0xffffffffu, 0x00020000);
+#ifdef CZ_DIAG_NOSTORE_ALL  // timing diagnostic only: every emitter's line stores dropped (wrong output)
+    if (v.x == 0x13579bdfu && v.w == 0x2468ace0u)
+#endif
     __builtin_amdgcn_raw_buffer_store_b128(v4u_t{v.x, v.y, v.z, v.w}, rs, (int)voff, 0, CP);
 }
 

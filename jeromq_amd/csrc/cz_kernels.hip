@@ -2858,16 +2858,17 @@ __global__ __launch_bounds__(BLOCK) CZ_OPEN_CARRY_OCC void k_open_uniform_carry(
         }
     }
     const bool un0 = allow_un0 && wave_uniform(INA >= 8 ? *reinterpret_cast<const u32 *>(src + 8) : ld32<false>(src + 8));
-    EmitLines em{smem + (threadIdx.x >> 6) * (LINE_LDS_BYTES / 16), out + (uint64_t)first * out_stride, dst,
-                 (uint64_t)P * out_stride, lane, nout, 0u, false};
+    using EmL = EmitLinesT<INA == 8 ? CZ_OPEN_STORE_CPOL : CZ_OPEN_ANY_STORE_CPOL>;
+    EmL em{smem + (threadIdx.x >> 6) * (LINE_LDS_BYTES / 16), out + (uint64_t)first * out_stride, dst,
+           (uint64_t)P * out_stride, lane, nout, 0u, false};
     u32 fl = 0;
     u64 nonce = 0;
     u32 st;
     if (un0)
-        st = open_frame<MODE_ZMQ, true, EmitLines, true, true, true, INA, true>(src, size, key, check != 0, floor, &fl,
+        st = open_frame<MODE_ZMQ, true, EmL, true, true, true, INA, true>(src, size, key, check != 0, floor, &fl,
                                                                             &nonce, 0, em);
     else
-        st = open_frame<MODE_ZMQ, true, EmitLines, true, false, true, INA, true>(src, size, key, check != 0, floor, &fl,
+        st = open_frame<MODE_ZMQ, true, EmL, true, false, true, INA, true>(src, size, key, check != 0, floor, &fl,
                                                                              &nonce, 0, em);
     status[i] = (uint16_t)(st | (st == CZ_STATUS_OK ? (fl << 8) : 0u));
 }
@@ -3769,7 +3770,9 @@ hipError_t czk_open_uniform(const void *in, uint64_t in_stride, void *out, uint6
     }
     // (INA 1 -- any byte offset -- measured 1.3% slower with carried lines at 2 waves per SIMD than
     // the straddling loads at 3, so only 8-byte aligned bodies take it: +2.6%)
-    if (g_pair && st_out == ST_LINES && ina == 8 && g_open_ina && g_open_carry && nout >= 256u) {
+    // (cz_tune("open_carry", 2): INA 1 too, A/B only)
+    if (g_pair && st_out == ST_LINES && (ina == 8 || (ina == 1 && g_open_carry == 2)) && g_open_ina && g_open_carry &&
+        nout >= 256u) {
         // phase-sorted waves with carried aligned lines (k_open_uniform_carry): whole blocks of 64 P
         // frames, P = the period of the bodies' line phase; the rest through k_open_uniform
         uint64_t g = in_stride & 127u, m = 128u;
@@ -3783,9 +3786,14 @@ hipError_t czk_open_uniform(const void *in, uint64_t in_stride, void *out, uint6
         if (blocks > 0 && 64ull * P * out_stride < (1ull << 31)) {
             const uint32_t nwaves = (uint32_t)(blocks * P);
             const dim3 cgrid((nwaves + WAVES - 1) / WAVES);
-            hipLaunchKernelGGL((k_open_uniform_carry<8>), cgrid, dim3(BLOCK), WAVES * LINE_LDS_BYTES, s,
-                               (const uint8_t *)in, in_stride, (uint8_t *)out, out_stride, nwaves, P, size,
-                               (const uint8_t *)subkey, floor0, check, status, g_un0);
+            if (ina == 8)
+                hipLaunchKernelGGL((k_open_uniform_carry<8>), cgrid, dim3(BLOCK), WAVES * LINE_LDS_BYTES, s,
+                                   (const uint8_t *)in, in_stride, (uint8_t *)out, out_stride, nwaves, P, size,
+                                   (const uint8_t *)subkey, floor0, check, status, g_un0);
+            else
+                hipLaunchKernelGGL((k_open_uniform_carry<1>), cgrid, dim3(BLOCK), WAVES * LINE_LDS_BYTES, s,
+                                   (const uint8_t *)in, in_stride, (uint8_t *)out, out_stride, nwaves, P, size,
+                                   (const uint8_t *)subkey, floor0, check, status, g_un0);
             const uint64_t done = blocks * 64ull * P;
             if (done < count) {
                 hipError_t e = hipGetLastError();
@@ -3795,9 +3803,14 @@ hipError_t czk_open_uniform(const void *in, uint64_t in_stride, void *out, uint6
                 const dim3 tgrid((rest + BLOCK - 1) / BLOCK);
                 const uint8_t *tin = (const uint8_t *)in + done * in_stride;
                 uint8_t *tout = (uint8_t *)out + done * out_stride;
-                hipLaunchKernelGGL((k_open_uniform<ST_LINES, true, 8>), tgrid, dim3(BLOCK), WAVES * LINE_LDS_BYTES,
-                                   s, tin, in_stride, tout, out_stride, rest, size, (const uint8_t *)subkey, floor0,
-                                   check, status + done, g_un0, 1);
+                if (ina == 8)
+                    hipLaunchKernelGGL((k_open_uniform<ST_LINES, true, 8>), tgrid, dim3(BLOCK), WAVES * LINE_LDS_BYTES,
+                                       s, tin, in_stride, tout, out_stride, rest, size, (const uint8_t *)subkey, floor0,
+                                       check, status + done, g_un0, 1);
+                else
+                    hipLaunchKernelGGL((k_open_uniform<ST_LINES, true, 1>), tgrid, dim3(BLOCK), WAVES * LINE_LDS_BYTES,
+                                       s, tin, in_stride, tout, out_stride, rest, size, (const uint8_t *)subkey, floor0,
+                                       check, status + done, g_un0, 1);
             }
             return hipGetLastError();
         }
@@ -3953,7 +3966,7 @@ int czk_tune(const char *key, int value)
     }
     if (__builtin_strcmp(key, "open_carry") == 0) {
         int old = g_open_carry;
-        g_open_carry = value != 0;
+        g_open_carry = value < 0 ? 0 : value > 2 ? 2 : value;
         return old;
     }
     if (__builtin_strcmp(key, "shift16") == 0) {

@@ -248,14 +248,15 @@ def test_seal_uniform_unaligned_payloads(torch_dev, subkeys, n, in_stride, out_s
 
 @pytest.mark.parametrize("n,stride,base,tail", [(4096, 4129, 0, 37), (4096, 4129, 3, 0), (1024, 1064, 8, 21),
                                                 (4096, 4136, 8, 5), (512, 545, 1, 64 * 3 + 1), (2048, 2082, 2, 9)])
-@pytest.mark.parametrize("carry", [1, 0])
+@pytest.mark.parametrize("carry", [1, 2, 0])
 def test_open_uniform_phase_sorted_carry(torch_dev, subkeys, n, stride, base, tail, carry):
     """The phase-sorted open of 8-byte aligned bodies (k_open_uniform_carry, cz_tune "open_carry"):
     whole blocks of 64 P frames, P = the period of the bodies' line phase (16 for a 4136 or 1064-byte
     stride), every wave one phase with the aligned lines carried; the frames after the last whole
     block go to k_open_uniform, whose first frame takes its replay floor from the body before it.
     Bodies at odd byte offsets (strides 4129, 545, 2082: P = 128 / 128 / 64) keep the straddling
-    loads, so they check the knob leaves them alone and the partial-wave slot contract.  Tampered frames inside carry waves and in the tail report
+    loads unless the knob is 2 (carried lines for INA 1, an A/B option), so they check both paths
+    and the partial-wave slot contract.  Tampered frames inside carry waves and in the tail report
     CRYPTO with zeros; a replayed nonce on the first tail frame reports SEQUENCE; every other payload
     and flags byte comes back, with carry on and off."""
     torch, dev = torch_dev

@@ -64,7 +64,7 @@ def test_nontemporal_line_stores(line_stores, prefix):
 
 @pytest.mark.parametrize("prefix", [
     "_ZN12_GLOBAL__N_114k_open_uniformILi1ELb1ELi16E",     # aligned open, 4 KiB plaintext slots
-    "_ZN12_GLOBAL__N_120k_open_uniform_carry",             # carried-line open
+    "_ZN12_GLOBAL__N_120k_open_uniform_carryILi8E",        # carried-line open, 8-byte aligned bodies
 ])
 def test_default_policy_line_stores(line_stores, prefix):
     st = _kernel(line_stores, prefix)

@@ -662,6 +662,30 @@ def nacl_latency(args, dev):
             t_s = med(lambda: sod.crypto_box_afternm(cs, m, ctypes.c_ulonglong(mlen), nonce, k), 2000)
             row["libsodium_1core_us"] = round(t_s * 1e6, 2)
         rows.append(row)
+    # boxes past one pass of k_nacl_one (80 KiB): the segment kernels (CurveZMQ boxes, m[0:32] == 0,
+    # the default) against k_nacl_one's multi-pass walk (cz_tune "nacl_one_max"; always taken by a
+    # seal whose m[0:32] is not zero, whose MAC key only k_nacl_one derives)
+    large = []
+    for n in (96 << 10, 256 << 10, 1 << 20, 4 << 20):
+        mlen = n + 32
+        m = (ctypes.c_uint8 * mlen)()
+        m[32:] = list(np.random.default_rng(n).integers(0, 256, size=n, dtype=np.uint8))
+        mp = (ctypes.c_uint8 * mlen).from_buffer_copy(bytes(range(1, 33)) + bytes(m)[32:])
+        c = (ctypes.c_uint8 * mlen)()
+        back = (ctypes.c_uint8 * mlen)()
+        row = {"box_bytes": mlen}
+        for name, knob in (("segments", 80 << 10), ("one_launch", 1 << 30)):
+            old = lib.cz_tune(b"nacl_one_max", knob)
+            try:
+                row[name + "_seal_us"] = round(med(lambda: lib.cz_box_afternm(c, m, mlen, nonce, k), 50) * 1e6, 1)
+                ok = bytes(c) == orc_seal(orc, bytes(m), nonce, k)
+                row[name + "_open_us"] = round(med(lambda: lib.cz_box_open_afternm(back, c, mlen, nonce, k), 50) * 1e6, 1)
+                row[name + "_verified"] = bool(ok and bytes(back) == bytes(m))
+            finally:
+                lib.cz_tune(b"nacl_one_max", old)
+        row["nonzero_prefix_seal_us"] = round(med(lambda: lib.cz_box_afternm(c, mp, mlen, nonce, k), 50) * 1e6, 1)
+        row["nonzero_prefix_verified"] = bytes(c) == orc_seal(orc, bytes(mp), nonce, k)
+        large.append(row)
     # the Mechanism mirror (cz_mech_encode / decode), one MESSAGE per call
     from jeromq_amd.mechanism import CurveClientMechanism, CurveServerMechanism, Msg
     mrows = []
@@ -699,7 +723,8 @@ def nacl_latency(args, dev):
     win = next((b["batch"] for b in batches if b["per_msg_us"] < ref_us), None)
     return {"metric": "jnacl drop-in single-message latency (cz_box_afternm / open), host buffers",
             "value": rows[1]["seal_us"], "unit": "us per 4 KiB message", "higher_is_better": False, "n_gpus": 1,
-            "ctypes_call_overhead_us": round(t_ctypes * 1e6, 2), "single_shot": rows, "mechanism_single": mrows,
+            "ctypes_call_overhead_us": round(t_ctypes * 1e6, 2), "single_shot": rows, "large_boxes": large,
+            "mechanism_single": mrows,
             "batched_4k": batches,
             "batch_beating_one_cpu_core": win,
             "cpu_reference_for_crossover": "libsodium crypto_box_afternm, 1 core" if sod is not None else "oracle, 1 core"}

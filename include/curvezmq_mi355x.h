@@ -101,10 +101,14 @@ typedef struct cz_frame_desc {
  * Replaces curve25519xsalsa20poly1305.crypto_box_afternm (called at Curve.java:136)
  * and crypto_box_open_afternm (Curve.java:146); crypto_secretbox[_open]
  * (xsalsa20poly1305, Curve.java:166,176) is the same primitive.
- * m[0:32] must be zero (NaCl's ZEROBYTES contract; a seal returns -1 otherwise rather than
- * produce different bytes); c[0:16] is written as zero.  Runs on the GPU in one launch per call
- * (boxes up to 80 KiB; larger ones through the segmented kernels): latency-bound, ~11 us of
- * launch + sync floor -- use the batched API for throughput. */
+ * NaCl's crypto_secretbox for every m, as jnacl and libsodium: c = keystream ^ m over all mlen
+ * bytes, the Poly1305 key is c[0:32] = keystream[0:32] ^ m[0:32] (so an m whose first 32 bytes
+ * are not zero -- Curve.box, Curve.java:184-193, accepts any m -- gets NaCl's tag, not an error),
+ * the tag lands at c[16:32] and c[0:16] is written as zero.  The open keys the MAC with the
+ * keystream (crypto_secretbox_open), returns -1 on a bad tag with m untouched, and writes
+ * m[0:32] as zero.  Runs on the GPU in one launch per call (every seal whose m[0:32] is not zero,
+ * and boxes up to 80 KiB; larger CurveZMQ boxes through the segmented kernels): latency-bound,
+ * ~11 us of launch + sync floor -- use the batched API for throughput. */
 int cz_box_afternm(uint8_t *c, const uint8_t *m, uint64_t mlen, const uint8_t n[24], const uint8_t k[32]);
 int cz_box_open_afternm(uint8_t *m, const uint8_t *c, uint64_t clen, const uint8_t n[24], const uint8_t k[32]);
 /* The one-launch drop-ins above keep, per calling thread, the HSalsa20 subkeys of the last 8
@@ -112,6 +116,11 @@ int cz_box_open_afternm(uint8_t *m, const uint8_t *c, uint64_t clen, const uint8
  * calls on a connection skip the derivation.  Wipe this thread's cache (host copy of the keys and
  * the device subkeys). */
 int cz_nacl_forget(void);
+/* Create the calling thread's single-shot contexts (the drop-ins' HIP stream, device buffers and
+ * pinned staging, and the handshake calls') now instead of on its first call.  Optional; the JNI
+ * shim calls it once per thread before it pins any Java array, so HIP runtime initialisation never
+ * runs while the JVM's GC is locked out (GetPrimitiveArrayCritical).  CZ_OK or CZ_EHIP. */
+int cz_nacl_thread_init(void);
 int cz_secretbox(uint8_t *c, const uint8_t *m, uint64_t mlen, const uint8_t n[24], const uint8_t k[32]);
 int cz_secretbox_open(uint8_t *m, const uint8_t *c, uint64_t clen, const uint8_t n[24], const uint8_t k[32]);
 
@@ -234,9 +243,11 @@ int cz_ctx_seal_uniform(cz_ctx *ctx, uint32_t count, uint32_t len, const void *h
                         uint64_t out_stride, uint64_t counter0, const uint8_t *h_flags8, uint32_t chunk_frames);
 int cz_ctx_open_uniform(cz_ctx *ctx, uint32_t count, uint32_t size, const void *h_in, uint64_t in_stride, void *h_out,
                         uint64_t out_stride, uint64_t floor0, int check, uint16_t *h_status, uint32_t chunk_frames);
-/* pinned host buffers for zero-extra-copy callers (a pinned MsgAllocator, zmq/msg/MsgAllocator.java:5-8) */
+/* pinned host buffers for zero-extra-copy callers (a pinned MsgAllocator, zmq/msg/MsgAllocator.java:5-8).
+ * cz_host_free frees only a base address cz_host_alloc returned and not yet freed (CZ_OK); any
+ * other pointer -- an interior address, foreign memory, a second free -- is CZ_EINVAL and left alone. */
 void *cz_host_alloc(uint64_t bytes);
-void cz_host_free(void *p);
+int cz_host_free(void *p);
 
 /* ---- 5. CURVE mechanism objects (host mirror of CurveClientMechanism / CurveServerMechanism
  *         in the CONNECTED state: encode/decode of MESSAGE commands with nonce bookkeeping) ---- */

@@ -116,7 +116,8 @@ SIGNATURES = {
     "cz_ctx_seal_uniform": (_I, [_VP, _U32, _U32, _VP, _U64, _VP, _U64, _U64, _VP, _U32]),
     "cz_ctx_open_uniform": (_I, [_VP, _U32, _U32, _VP, _U64, _VP, _U64, _U64, _I, _VP, _U32]),
     "cz_host_alloc": (_VP, [_U64]),
-    "cz_host_free": (None, [_VP]),
+    "cz_host_free": (_I, [_VP]),
+    "cz_nacl_thread_init": (_I, []),
     "cz_mech_create": (_VP, [_I, _VP, _U64, _U64, _I]),
     "cz_mech_destroy": (None, [_VP]),
     "cz_mech_encode": (ctypes.c_int64, [_VP, _VP, _U64, _I, _VP]),

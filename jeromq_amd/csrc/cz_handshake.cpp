@@ -66,6 +66,8 @@ int hs_one(uint8_t out[32], const uint8_t scalar[32], const uint8_t *point, int 
 
 }  // namespace
 
+int czi::hs_thread_init() { return hs_init(); }
+
 extern "C" {
 
 int cz_scalarmult(uint8_t q[32], const uint8_t n[32], const uint8_t p[32])
@@ -105,7 +107,7 @@ int cz_box(uint8_t *c, const uint8_t *m, uint64_t mlen, const uint8_t n[24], con
     if (cz_box_beforenm(k, pk, sk) != 0)
         return -1;
     int rc = cz_box_afternm(c, m, mlen, n, k);
-    memset(k, 0, sizeof(k));
+    explicit_bzero(k, sizeof(k));
     return rc;
 }
 
@@ -116,7 +118,7 @@ int cz_box_open(uint8_t *m, const uint8_t *c, uint64_t clen, const uint8_t n[24]
     if (cz_box_beforenm(k, pk, sk) != 0)
         return -1;
     int rc = cz_box_open_afternm(m, c, clen, n, k);
-    memset(k, 0, sizeof(k));
+    explicit_bzero(k, sizeof(k));
     return rc;
 }
 

@@ -8,8 +8,10 @@
 #include <algorithm>
 #include <cstdio>
 #include <cstring>
+#include <mutex>
 #include <numeric>
 #include <string>
+#include <unordered_set>
 #include <vector>
 
 #include "../../include/curvezmq_mi355x.h"
@@ -26,7 +28,6 @@ hipError_t czk_open_desc(const cz_frame_desc *, const uint32_t *, uint32_t, cons
                          uint16_t *, uint64_t *, hipStream_t);
 hipError_t czk_open_uniform(const void *, uint64_t, void *, uint64_t, uint32_t, uint32_t, const void *, uint64_t, int,
                             uint16_t *, hipStream_t);
-hipError_t czk_box_nacl(const void *, void *, uint32_t, const void *, uint64_t, int, int *, hipStream_t);
 hipError_t czk_fill(void *, uint64_t, uint64_t, hipStream_t);
 hipError_t czk_copy16(void *, const void *, uint64_t, hipStream_t);
 int czk_tune(const char *, int);
@@ -105,11 +106,10 @@ void HostBuf::release()
 }
 
 // ---- per-thread single-shot context ----------------------------------------
-// One message per call (the jnacl drop-ins).  Messages of more than a few blocks run through the
-// segment planner and kernels, so a 64 KiB box spreads over ~130 lanes instead of walking 1025
-// Salsa20 blocks on one lane (k_box_nacl keeps only mlen == 32, which has no MESSAGE form).
-// Everything the device needs -- key, descriptor, segment and combine lists, the message -- goes
-// over in ONE pinned H2D copy, and the result in one D2H copy.
+// One message per call (the jnacl drop-ins).  Boxes above 80 KiB run through the segment planner
+// and kernels, so a long box spreads over many workgroups: everything the device needs -- key,
+// descriptor, segment and combine lists, the message -- goes over in ONE pinned H2D copy, and the
+// result in one D2H copy.
 // One-launch path (k_nacl_one): the staging is pinned host memory the kernel reads and writes
 // directly, and the subkey HSalsa20(k, n[0:16]) of the last NCACHE (k, n[0:16]) pairs this thread
 // used stays in device memory (CurveZMQ: one pair per connection direction).  cz_nacl_forget()
@@ -137,6 +137,10 @@ struct Single {
 
 static thread_local Single t_single;
 
+// base addresses cz_host_alloc handed out and cz_host_free has not released
+static std::mutex g_host_mu;
+static std::unordered_set<void *> g_host_bases;
+
 static int single_init()
 {
     if (t_single.ready)
@@ -156,10 +160,24 @@ static int single_init()
 
 static uint64_t up128(uint64_t v) { return (v + 127) & ~127ull; }
 
+// Bytes a uniform batch spans from its base, (count - 1) * stride + last, if that fits in 2^47 (a
+// canonical user address range: no stride makes frame i's address wrap, and count * stride sums of
+// the staging sizes stay far from 2^64); false otherwise.
+static bool uniform_span(uint32_t count, uint64_t stride, uint64_t last, uint64_t *bytes)
+{
+    uint64_t v = 0;
+    if (count && (__builtin_mul_overflow((uint64_t)(count - 1), stride, &v) || __builtin_add_overflow(v, last, &v)))
+        return false;
+    if (v > (1ull << 47))
+        return false;
+    if (bytes)
+        *bytes = v;
+    return true;
+}
+
 // NaCl box/open of one message in ONE launch (k_nacl_one): input staged into pinned host memory
 // the kernel reads directly, output read back from it after the launch.  -1 on a bad tag (dst
-// untouched) or a seal whose m[0:32] is not zero (NaCl's crypto_box_afternm contract: the MAC key
-// is c[0:32] = keystream ^ m[0:32], which the device path keeps as the keystream alone).
+// untouched).  The seal is NaCl's for every m: the MAC key is c[0:32] = keystream ^ m[0:32].
 static int nacl_one_launch(uint8_t *dst, const uint8_t *src, uint64_t len, const uint8_t n[24], const uint8_t k[32],
                            int open)
 {
@@ -191,8 +209,9 @@ static int nacl_one_launch(uint8_t *dst, const uint8_t *src, uint64_t len, const
     if ((e = czk_nacl_one(st, (uint32_t)len, open, (uint8_t *)s.subcache.ptr + 32 * slot, miss, (uint32_t)out_off, k, n,
                           s.stream)) != hipSuccess ||
         (e = hipStreamSynchronize(s.stream)) != hipSuccess) {
-        if (!open)
-            explicit_bzero(st + 128, len);  // the staged plaintext box (as Mechanism::seal_one)
+        // no plaintext left in the pinned staging on a failed call: the staged box (seal) or
+        // whatever part of m the kernel wrote before the failure (open)
+        explicit_bzero(open ? st + out_off : st + 128, len);
         hip_fail(e, "cz_box (one launch)");
         return -1;
     }
@@ -201,9 +220,11 @@ static int nacl_one_launch(uint8_t *dst, const uint8_t *src, uint64_t len, const
     const int rc = *(volatile int *)(st + 56);
     if (!open) {
         explicit_bzero(st + 128, len);  // no plaintext left in the pinned staging after the call
+        if (rc != 0)
+            return fail(CZ_EHIP, "cz_box (one launch): the kernel did not complete"), -1;
         memset(dst, 0, 16);
         memcpy(dst + 16, st + out_off + 16, len - 16);
-        return rc == 0 ? 0 : -1;
+        return 0;
     }
     if (rc != 0) {
         explicit_bzero(st + out_off, len);  // never leave unauthenticated plaintext behind
@@ -215,6 +236,17 @@ static int nacl_one_launch(uint8_t *dst, const uint8_t *src, uint64_t len, const
     return 0;
 }
 
+// Boxes above this many bytes whose MAC key is the keystream alone (every open, and every seal
+// with m[0:32] == 0, i.e. every CurveZMQ box) run on the segment kernels, which spread a long box
+// over many workgroups; smaller boxes, and seals whose m[0:32] is not zero (the MAC key is then
+// keystream ^ m[0:32], which only k_nacl_one derives), take one launch.  Measured on MI355X
+// (bench.py --config nacl, "large_boxes"; profiles/r05/nacl_large_boxes.json): one launch / segments
+// seal 57 / 166 us at 96 KiB, 114 / 254 at 256 KiB, 380 / 471 at 1 MiB, 1330 / 1174 at 4 MiB.
+// cz_tune("nacl_one_max") moves the edge; the Mechanism mirror uses the same one.
+static uint64_t g_nacl_one_bytes = 2ull << 20;
+
+uint64_t nacl_one_bytes() { return std::max<uint64_t>(g_nacl_one_bytes, czk_nacl_one_max()); }
+
 // NaCl box/open of one message on the device.  A MESSAGE is the NaCl box of
 // 0^32 || flags || payload, so m[32] rides as the flags byte and m[33:] as the payload; for open
 // the 16 bytes ahead of the tag are rebuilt as "\x07MESSAGE" || n[16:24] and the nonce check is off.
@@ -225,51 +257,26 @@ static int nacl_one(uint8_t *dst, const uint8_t *src, uint64_t len, const uint8_
         return -1;
     if (len < 32 || len > 0xffffffffull)
         return -1;
-    if (!open) {  // crypto_box_afternm's contract: m starts with 32 zero bytes
+    if (single_init() != CZ_OK)
+        return -1;
+    bool one = len <= nacl_one_bytes();
+    if (!one && !open) {
         uint8_t z = 0;
         for (int i = 0; i < 32; i++)
             z |= src[i];
-        if (z)
-            return fail(CZ_EINVAL, "cz_box_afternm: m[0:32] is not zero (NaCl ZEROBYTES)"), -1;
+        one = z != 0;
     }
-    if (single_init() != CZ_OK)
-        return -1;
-    static const bool segmented_only = getenv("CZ_NACL_SEGMENTED") != nullptr;  // A/B: the multi-launch path
-    if (len <= czk_nacl_one_max() && !segmented_only)
+    if (one) {
+        if (len > czk_nacl_one_limit())
+            return fail(CZ_EINVAL, "cz_box_afternm: a box with m[0:32] != 0 is limited to %u bytes",
+                        czk_nacl_one_limit()), -1;
         return nacl_one_launch(dst, src, len, n, k, open);
+    }
     Single &s = t_single;
     uint64_t counter = 0;
     for (int i = 0; i < 8; i++)
         counter = (counter << 8) | n[16 + i];
     hipError_t e;
-    if (len == 32) {  // empty box: no flags byte, so no MESSAGE form; one lane of k_box_nacl
-        uint8_t *st = nullptr;
-        if ((e = s.dev.reserve(256)) != hipSuccess || (e = s.stage.reserve(256)) != hipSuccess) {
-            hip_fail(e, "alloc");
-            return -1;
-        }
-        st = (uint8_t *)s.stage.ptr;
-        uint8_t *d = (uint8_t *)s.dev.ptr;
-        memcpy(st, k, 32);
-        memcpy(st + 128, src, 32);
-        int rc = -1;
-        if ((e = hipMemcpyAsync(d, st, 160, hipMemcpyHostToDevice, s.stream)) != hipSuccess ||
-            (e = czk_subkeys(d, d + 32, 1, n, s.stream)) != hipSuccess ||
-            (e = czk_box_nacl(d + 128, d + 192, 32, d + 32, counter, open, (int *)s.rc.ptr, s.stream)) != hipSuccess ||
-            (e = hipMemcpyAsync(st + 192, d + 192, 32, hipMemcpyDeviceToHost, s.stream)) != hipSuccess ||
-            (e = hipMemcpyAsync(&rc, s.rc.ptr, sizeof(int), hipMemcpyDeviceToHost, s.stream)) != hipSuccess ||
-            (e = hipMemsetAsync(d, 0, 64, s.stream)) != hipSuccess ||  // no key material left behind
-            (e = hipStreamSynchronize(s.stream)) != hipSuccess) {
-            memset(st, 0, 32);
-            hip_fail(e, "box");
-            return -1;
-        }
-        memset(st, 0, 32);
-        if (rc != 0)
-            return -1;
-        memcpy(dst, st + 192, 32);
-        return 0;
-    }
     // one descriptor, its segments and combine record
     cz_frame_desc d{};
     d.key_idx = 0;
@@ -329,24 +336,33 @@ static int nacl_one(uint8_t *dst, const uint8_t *src, uint64_t len, const uint8_
         (e = hipMemsetAsync(dv, 0, 64, s.stream)) != hipSuccess ||  // no key material left behind
         (e = hipMemcpyAsync(st + 128, dv + 128, 2, hipMemcpyDeviceToHost, s.stream)) != hipSuccess ||
         (e = hipMemcpyAsync(st + o_out, dv + o_out, out_bytes, hipMemcpyDeviceToHost, s.stream)) != hipSuccess ||
+        // nor plaintext: the staged payload (seal) or the opened one (open), on the device
+        (e = hipMemsetAsync(dv + (open ? o_out : o_in), 0, open ? out_bytes : in_bytes, s.stream)) != hipSuccess ||
         (e = hipStreamSynchronize(s.stream)) != hipSuccess) {
-        memset(st, 0, 32);
+        (void)hipStreamSynchronize(s.stream);
+        explicit_bzero(st, 32);
+        explicit_bzero(st + o_in, in_bytes);
+        explicit_bzero(st + o_out, out_bytes);
         hip_fail(e, "box");
         return -1;
     }
-    memset(st, 0, 32);
+    explicit_bzero(st, 32);
     if (!open) {
+        explicit_bzero(st + o_in, in_bytes);
         memset(dst, 0, 16);
         memcpy(dst + 16, st + o_out + 16, len - 16);
         return 0;
     }
     uint16_t status;
     memcpy(&status, st + 128, 2);
-    if ((status & 0xff) != CZ_STATUS_OK)
+    if ((status & 0xff) != CZ_STATUS_OK) {
+        explicit_bzero(st + o_out, out_bytes);
         return -1;  // tag mismatch: dst untouched (as NaCl)
+    }
     memset(dst, 0, 32);
     dst[32] = (uint8_t)(status >> 8);
     memcpy(dst + 33, st + o_out, out_bytes);
+    explicit_bzero(st + o_out, out_bytes);
     return 0;
 }
 
@@ -462,6 +478,11 @@ const char *cz_version(void) { return "curvezmq-mi355x 0.1 (gfx950)"; }
 
 int cz_tune(const char *key, int value)
 {
+    if (key && strcmp(key, "nacl_one_max") == 0) {  // bytes; at least one pass of k_nacl_one
+        const int old = (int)g_nacl_one_bytes;
+        g_nacl_one_bytes = std::min<uint64_t>(std::max<int64_t>(value, 0), czk_nacl_one_limit());
+        return old;
+    }
     int old = czk_tune(key, value);
     if (old < 0)
         return fail(CZ_EINVAL, "cz_tune: unknown key");
@@ -575,6 +596,9 @@ int cz_seal_uniform(uint32_t count, uint32_t len, const void *d_in, uint64_t in_
         return fail(CZ_EINVAL, "cz_seal_uniform: stride smaller than the frame");
     if ((uint64_t)len + CZ_MESSAGE_OVERHEAD > 0xffffffffull)
         return fail(CZ_EINVAL, "cz_seal_uniform: frame too large");
+    if (!uniform_span(count, in_stride, len, nullptr) ||
+        !uniform_span(count, out_stride, (uint64_t)len + CZ_MESSAGE_OVERHEAD, nullptr))
+        return fail(CZ_EINVAL, "cz_seal_uniform: count x stride overflows the address space");
     hipError_t e = czk_seal_uniform(d_in, in_stride, d_out, out_stride, count, len, d_subkey, counter0, d_flags8,
                                     (hipStream_t)stream);
     return e == hipSuccess ? CZ_OK : hip_fail(e, "cz_seal_uniform");
@@ -589,6 +613,9 @@ int cz_seal_uniform_box(uint32_t count, uint32_t len, const void *d_box, uint64_
         return fail(CZ_EINVAL, "cz_seal_uniform_box: frame too large");
     if (count > 1 && (box_stride < (uint64_t)len + CZ_MESSAGE_OVERHEAD || out_stride < (uint64_t)len + CZ_MESSAGE_OVERHEAD))
         return fail(CZ_EINVAL, "cz_seal_uniform_box: stride smaller than the frame");
+    if (!uniform_span(count, box_stride, (uint64_t)len + CZ_MESSAGE_OVERHEAD, nullptr) ||
+        !uniform_span(count, out_stride, (uint64_t)len + CZ_MESSAGE_OVERHEAD, nullptr))
+        return fail(CZ_EINVAL, "cz_seal_uniform_box: count x stride overflows the address space");
     hipError_t e = czk_seal_uniform_box(d_box, box_stride, d_out, out_stride, count, len, d_subkey, counter0,
                                         (hipStream_t)stream);
     return e == hipSuccess ? CZ_OK : hip_fail(e, "cz_seal_uniform_box");
@@ -602,6 +629,9 @@ int cz_open_uniform(uint32_t count, uint32_t size, const void *d_in, uint64_t in
         return fail(CZ_EINVAL, "cz_open_uniform: null pointer");
     if (count > 1 && (in_stride < size || (size >= 33 && out_stride < size - 33u)))
         return fail(CZ_EINVAL, "cz_open_uniform: stride smaller than the frame");
+    if (!uniform_span(count, in_stride, size, nullptr) ||
+        !uniform_span(count, out_stride, size >= 33 ? size - 33u : 0u, nullptr))
+        return fail(CZ_EINVAL, "cz_open_uniform: count x stride overflows the address space");
     hipError_t e = czk_open_uniform(d_in, in_stride, d_out, out_stride, count, size, d_subkey, floor0, check,
                                     d_status, (hipStream_t)stream);
     return e == hipSuccess ? CZ_OK : hip_fail(e, "cz_open_uniform");
@@ -942,6 +972,9 @@ static int ctx_uniform(cz_ctx *c, bool seal, uint32_t count, uint32_t len, const
     const uint64_t olen = seal ? (uint64_t)len + CZ_MESSAGE_OVERHEAD : (len >= 33 ? len - 33u : 0u);
     if (count > 1 && (in_stride < len || out_stride < olen))
         return fail(CZ_EINVAL, "cz_ctx_*_uniform: stride smaller than a frame");
+    // the staging sizes below are count * stride products: refuse strides they would wrap
+    if (count > 1 && (!uniform_span(count, in_stride, len, nullptr) || !uniform_span(count, out_stride, olen, nullptr)))
+        return fail(CZ_EINVAL, "cz_ctx_*_uniform: count x stride overflows the address space");
     if (count == 0)
         return CZ_OK;
     if (count == 1) {  // strides are not checked for one frame: its slot is the frame itself
@@ -950,8 +983,7 @@ static int ctx_uniform(cz_ctx *c, bool seal, uint32_t count, uint32_t len, const
     }
     // a single-chunk batch of multi-block frames: the segment kernels (one stream)
     const uint64_t nblk = ((seal ? (uint64_t)len + CZ_MESSAGE_OVERHEAD : (uint64_t)len) + 63) / 64;
-    static const bool lanes_only = getenv("CZ_CTX_LANES_ONLY") != nullptr;  // A/B: the lane-per-frame kernel
-    const bool seg_path = nblk >= 8 && (chunk == 0 || chunk >= count) && !lanes_only &&
+    const bool seg_path = nblk >= 8 && (chunk == 0 || chunk >= count) &&
                           (uint64_t)count * (in_stride + out_stride) <= SEG_BATCH_BYTES;
     // (default chunks of count / 8 within 2048 .. 16384 frames were slower than 16384 for every
     // batch of 8192 .. 65536 x 4 KiB: profiles/r03/ctx_small_batch.log)
@@ -1065,13 +1097,30 @@ void *cz_host_alloc(uint64_t bytes)
         fail(CZ_ENOMEM, "hipHostMalloc(%llu) failed", (unsigned long long)bytes);
         return nullptr;
     }
+    std::lock_guard<std::mutex> g(g_host_mu);
+    g_host_bases.insert(p);
     return p;
 }
 
-void cz_host_free(void *p)
+int cz_host_free(void *p)
 {
-    if (p)
-        (void)hipHostFree(p);
+    if (!p)
+        return CZ_OK;
+    {
+        std::lock_guard<std::mutex> g(g_host_mu);
+        if (g_host_bases.erase(p) == 0)
+            return fail(CZ_EINVAL, "cz_host_free: %p is not a live cz_host_alloc base address", p);
+    }
+    hipError_t e = hipHostFree(p);
+    return e == hipSuccess ? CZ_OK : hip_fail(e, "cz_host_free");
+}
+
+int cz_nacl_thread_init(void)
+{
+    int rc = single_init();
+    if (rc == CZ_OK)
+        rc = hs_thread_init();
+    return rc;
 }
 
 }  // extern "C"

@@ -21,11 +21,14 @@ hipError_t czk_open_segments(const cz_frame_desc *, const cz_segment *, uint32_t
 hipError_t czk_v2_copy(const cz_v2_item *, uint32_t, const void *, void *, hipStream_t);
 hipError_t czk_nacl_one(void *, uint32_t, int, void *, int, uint32_t, const uint8_t *, const uint8_t *, hipStream_t);
 uint32_t czk_nacl_one_max(void);
+uint32_t czk_nacl_one_limit(void);
 }
 
 namespace czi {
 
 int fail(int code, const char *fmt, ...);
+int hs_thread_init();  // the calling thread's handshake context (cz_handshake.cpp)
+uint64_t nacl_one_bytes();  // boxes up to this size take k_nacl_one (cz_tune "nacl_one_max")
 int hip_fail(hipError_t e, const char *where);
 const uint8_t *prefix_for(int direction);
 void plan_segments(const cz_frame_desc *h_desc, uint32_t count, int open, uint32_t seg_blocks,

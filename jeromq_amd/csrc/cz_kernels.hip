@@ -3268,44 +3268,6 @@ __global__ __launch_bounds__(BLOCK) void k_v2_copy(const cz_v2_item *__restrict_
     }
 }
 
-// NaCl-layout single frame (jnacl crypto_box_afternm / crypto_box_open_afternm drop-in).
-// params: subkey (32 B device), counter = BE64(n[16:24]).
-__global__ __launch_bounds__(64) void k_box_nacl(const uint8_t *__restrict__ in, uint8_t *__restrict__ out,
-                                                  uint32_t len, const uint8_t *__restrict__ subkey,
-                                                  uint64_t counter, int open, int *__restrict__ rc)
-{
-    if (threadIdx.x != 0 || blockIdx.x != 0)
-        return;
-    u32 key[8];
-    load_key(subkey, key);
-    if (!open) {
-        if (len < 32u) {
-            *rc = -1;
-            return;
-        }
-        if (aligned16(in, out)) {
-            EmitDirect<true> em{out, len};
-            seal_frame<MODE_NACL, true>(in, len, 0u, counter, key, em);
-        } else {
-            EmitDirect<false> em{out, len};
-            seal_frame<MODE_NACL, false>(in, len, 0u, counter, key, em);
-        }
-        *rc = 0;
-    } else {
-        u32 fl;
-        u64 nonce;
-        u32 st;
-        if (aligned16(in, out)) {
-            EmitDirect<true> em{out, len};
-            st = open_frame<MODE_NACL, true>(in, len, key, false, 0, &fl, &nonce, counter, em);
-        } else {
-            EmitDirect<false> em{out, len};
-            st = open_frame<MODE_NACL, false>(in, len, key, false, 0, &fl, &nonce, counter, em);
-        }
-        *rc = st == CZ_STATUS_OK ? 0 : -1;
-    }
-}
-
 // ---- one NaCl box per launch (the jnacl crypto_box_afternm / open_afternm drop-ins) ----------
 // One call used to be a chain of copies and launches (subkey, segments, combine, wipe): ~50 us at
 // 4 KiB against ~11 us for a bare launch + sync (tools/diag/latency_ub.hip).  This kernel does the
@@ -3313,18 +3275,22 @@ __global__ __launch_bounds__(64) void k_box_nacl(const uint8_t *__restrict__ in,
 // output to the caller thread's pinned staging (host memory the device addresses directly):
 //   - the subkey HSalsa20(k, n[0:16]) comes from the thread's device cache, or is derived here and
 //     cached (CurveZMQ uses one (k, "CurveZMQMESSAGE?") pair per connection direction);
-//   - thread t owns box blocks [t*w, t*w + w) (w <= NACL_ONE_W): loads them, XORs its keystream,
-//     writes the output and keeps the ciphertext for the MAC;
-//   - Poly1305 over c[32:len) in parallel: each thread runs Horner over its own 16-byte blocks
-//     (box block b >= 1 holds MAC blocks 4b-2 .. 4b+1), the full threads' partials are joined by a
+//   - thread t owns box blocks [t*w, t*w + w), walked in passes of NACL_ONE_W blocks (one pass for
+//     boxes up to 80 KiB): loads them, XORs its keystream, writes the output and runs Horner over
+//     the pass's ciphertext;
+//   - the MAC key is NaCl's: crypto_secretbox keys Poly1305 with c[0:32] = keystream ^ m[0:32], so a
+//     seal whose m[0:32] is not zero (jnacl and libsodium accept it; Curve.box, Curve.java:184-193,
+//     reaches it) gets the same tag as theirs; crypto_secretbox_open keys it with the keystream;
+//   - Poly1305 over c[32:len) in parallel: each thread's Horner value over its own 16-byte blocks
+//     (box block b >= 1 holds MAC blocks 4b-2 .. 4b+1); the full threads 0..L-1 are joined by a
 //     pairwise tree with multipliers r^(Q*2^l), Q = 4w MAC blocks per thread (radix 2^26), and the
-//     thread holding the last block continues its Horner chain from the joined value.
+//     thread L holding the last block finishes H = G * r^(n_L) + A_L.
 // k and n come in the kernel arguments; staging layout (bytes): [56,60) rc (written here),
-// [128, 128 + len) input, [out_off, out_off + len) output.  Seal: bytes 0..31 of m are not read (the host checked they are 0)
-// and the output holds c[16:len) at out_off + 16; open: the output holds m[32:len) at out_off + 32,
-// released by the host only when rc == 0.
+// [128, 128 + len) input, [out_off, out_off + len) output.  Seal: the output holds c[16:len) at
+// out_off + 16; open: the output holds m[32:len) at out_off + 32, released by the host only when
+// rc == 0.
 constexpr int NACL_ONE_T = 256;
-constexpr int NACL_ONE_W = 5;  // blocks per thread: boxes up to 256 * 5 * 64 = 80 KiB
+constexpr int NACL_ONE_W = 5;  // blocks per thread and pass: one pass covers 256 * 5 * 64 = 80 KiB
 // k and n travel in the kernel arguments (the dispatch packet), not through host memory: the only
 // PCIe read on the critical path is the message itself, issued first
 struct NaclOneArgs {
@@ -3339,25 +3305,90 @@ __global__ __launch_bounds__(NACL_ONE_T) void k_nacl_one(uint8_t *st, uint32_t l
     __shared__ u32 s_tree[NACL_ONE_T * 5];
     const u32 t = threadIdx.x;
     const u32 nblk = (len + 63u) >> 6;
-    const u32 w = (nblk + NACL_ONE_T - 1) / NACL_ONE_T;
+    const u32 w = (nblk + NACL_ONE_T - 1) / NACL_ONE_T;  // blocks per thread
+    const u32 npass = (w + NACL_ONE_W - 1) / NACL_ONE_W;  // the same in every thread
     const u32 n0 = args.n[4], n1 = args.n[5];
     const u32 b0 = t * w;
+    const u32 bend = b0 + w < nblk ? b0 + w : nblk;      // <= b0 for the threads past the box
     const uint8_t *in = st + 128;
     uint8_t *out = st + out_off;
-    // 1. this thread's message blocks (host memory, over PCIe): loads issued before anything else
     u32 Cb[NACL_ONE_W][16];
+    // the pass's message blocks (host memory, over PCIe); the seal reads m[0:32] too (the MAC key)
+    auto load_pass = [&](u32 pb) {
 #pragma unroll
-    for (int j = 0; j < NACL_ONE_W; j++) {
-        const u32 b = b0 + (u32)j;
-        if ((u32)j >= w || b >= nblk)
-            continue;
+        for (int j = 0; j < NACL_ONE_W; j++) {
+            const u32 b = pb + (u32)j;
+            if (b >= bend)
+                continue;
 #pragma unroll
-        for (int c = 0; c < 4; c++) {
-            const u32 oc = 64u * b + 16u * c;
-            V4 v = (oc >= 32u) ? ld16<true>(in + oc, oc < len ? len - oc : 0) : zero4();
-            Cb[j][4 * c] = v.x; Cb[j][4 * c + 1] = v.y; Cb[j][4 * c + 2] = v.z; Cb[j][4 * c + 3] = v.w;
+            for (int c = 0; c < 4; c++) {
+                const u32 oc = 64u * b + 16u * c;
+                V4 v = (oc >= 32u || !open) ? ld16<true>(in + oc, oc < len ? len - oc : 0) : zero4();
+                Cb[j][4 * c] = v.x; Cb[j][4 * c + 1] = v.y; Cb[j][4 * c + 2] = v.z; Cb[j][4 * c + 3] = v.w;
+            }
         }
-    }
+    };
+    // keystream, XOR, output; Cb keeps the ciphertext for the MAC
+    auto xor_pass = [&](u32 pb, const u32 key[8]) {
+#pragma unroll
+        for (int j = 0; j < NACL_ONE_W; j++) {
+            const u32 b = pb + (u32)j;
+            if (b >= bend)
+                continue;
+            u32 x[16];
+            salsa20_block<false>(x, key, n0, n1, b, 0u);
+            const u32 o = 64u * b;
+            u32 M[16];
+#pragma unroll
+            for (int k = 0; k < 16; k++) {
+                M[k] = Cb[j][k] ^ x[k];  // output: c (seal) or m (open)
+                if (!open)
+                    Cb[j][k] = M[k];     // the MAC runs over the ciphertext
+            }
+            if (b == 0) {  // MAC key: c[0:32] (seal), the keystream (open)
+#pragma unroll
+                for (int i = 0; i < 8; i++) {
+                    const u32 kw = open ? x[i] : M[i];
+                    s_rs[i] = i >= 4 ? kw : kw & (i == 0 ? 0x0fffffffu : 0x0ffffffcu);
+                }
+            }
+            // output bytes [max(o, 32), min(o + 64, len)) (seal: bytes 16..31 are the tag, written below)
+#pragma unroll
+            for (int c = 0; c < 4; c++) {
+                const u32 oc = o + 16u * c;
+                if (oc >= 32u && oc < len) {
+                    const u32 cnt = len - oc < 16u ? len - oc : 16u;
+                    if (cnt == 16u)
+                        *reinterpret_cast<uint4 *>(out + oc) = make_uint4(M[4 * c], M[4 * c + 1], M[4 * c + 2], M[4 * c + 3]);
+                    else
+                        st_bytes(out + oc, M[4 * c], M[4 * c + 1], M[4 * c + 2], M[4 * c + 3], cnt);
+                }
+            }
+        }
+    };
+    Poly P;
+    // Horner over the pass's MAC blocks: p covers c[32 + 16p, 48 + 16p), the last one possibly partial
+    auto horner_pass = [&](u32 pb) {
+#pragma unroll
+        for (int j = 0; j < NACL_ONE_W; j++) {
+            const u32 b = pb + (u32)j;
+            if (b >= bend)
+                continue;
+#pragma unroll
+            for (int c = 0; c < 4; c++) {
+                const u32 oc = 64u * b + 16u * c;
+                if (oc < 32u || oc >= len)
+                    continue;
+                const u32 cnt = len - oc;
+                if (cnt >= 16u)
+                    poly_block(P, Cb[j][4 * c], Cb[j][4 * c + 1], Cb[j][4 * c + 2], Cb[j][4 * c + 3], 1u);
+                else
+                    poly_block_partial(P, Cb[j][4 * c], Cb[j][4 * c + 1], Cb[j][4 * c + 2], Cb[j][4 * c + 3], cnt);
+            }
+        }
+    };
+    // 1. the first pass's loads, issued before anything else
+    load_pass(b0);
     // 2. the subkey: wave 0 derives it (every lane the same HSalsa20; lane 0 caches it) or loads it
     if (t < 64) {
         u32 key[8];
@@ -3379,90 +3410,21 @@ __global__ __launch_bounds__(NACL_ONE_T) void k_nacl_one(uint8_t *st, uint32_t l
 #pragma unroll
     for (int i = 0; i < 8; i++)
         key[i] = s_key[i];
-    // 3. keystream, XOR, output; Cb keeps the ciphertext for the MAC
-#pragma unroll
-    for (int j = 0; j < NACL_ONE_W; j++) {
-        const u32 b = b0 + (u32)j;
-        if ((u32)j >= w || b >= nblk)
-            continue;
-        u32 x[16];
-        salsa20_block<false>(x, key, n0, n1, b, 0u);
-        if (b == 0) {
-#pragma unroll
-            for (int i = 0; i < 4; i++)
-                s_rs[i] = x[i] & (i == 0 ? 0x0fffffffu : 0x0ffffffcu);
-#pragma unroll
-            for (int i = 4; i < 8; i++)
-                s_rs[i] = x[i];
-        }
-        const u32 o = 64u * b;
-        u32 M[16];
-#pragma unroll
-        for (int k = 0; k < 16; k++) {
-            M[k] = Cb[j][k] ^ x[k];  // output: c (seal) or m (open)
-            if (!open)
-                Cb[j][k] = M[k];     // the MAC runs over the ciphertext
-        }
-        // output bytes [max(o, 32), min(o + 64, len)) (seal: bytes 16..31 are the tag, written below)
-#pragma unroll
-        for (int c = 0; c < 4; c++) {
-            const u32 oc = o + 16u * c;
-            if (oc >= 32u && oc < len) {
-                const u32 cnt = len - oc < 16u ? len - oc : 16u;
-                if (cnt == 16u)
-                    *reinterpret_cast<uint4 *>(out + oc) = make_uint4(M[4 * c], M[4 * c + 1], M[4 * c + 2], M[4 * c + 3]);
-                else
-                    st_bytes(out + oc, M[4 * c], M[4 * c + 1], M[4 * c + 2], M[4 * c + 3], cnt);
-            }
-        }
-    }
+    // 3. the first pass (block 0 gives the MAC key), then the rest with their MAC on the way
+    xor_pass(b0, key);
     __syncthreads();
-    Poly P;
     poly_init(P, s_rs[0], s_rs[1], s_rs[2], s_rs[3], s_rs[4], s_rs[5], s_rs[6], s_rs[7]);
-    // MAC blocks: p covers c[32 + 16p, 48 + 16p); NP of them, the last one possibly partial
-    const u32 mlen = len;
-    const u32 NP = mlen > 32u ? (mlen - 32u + 15u) >> 4 : 0u;
-    const u32 last_blk = nblk ? nblk - 1u : 0u;
-    const u32 L = last_blk / w;  // the thread holding the last box block
-    // Horner over this thread's MAC blocks, h = sum m_p r^(end - p)
-    auto horner = [&]() {
-#pragma unroll
-        for (int j = 0; j < NACL_ONE_W; j++) {
-            const u32 b = b0 + (u32)j;
-            if ((u32)j >= w || b >= nblk)
-                continue;
-#pragma unroll
-            for (int c = 0; c < 4; c++) {
-                const u32 oc = 64u * b + 16u * c;
-                if (oc < 32u || oc >= mlen)
-                    continue;
-                const u32 cnt = mlen - oc;
-                if (cnt >= 16u)
-                    poly_block(P, Cb[j][4 * c], Cb[j][4 * c + 1], Cb[j][4 * c + 2], Cb[j][4 * c + 3], 1u);
-                else
-                    poly_block_partial(P, Cb[j][4 * c], Cb[j][4 * c + 1], Cb[j][4 * c + 2], Cb[j][4 * c + 3], cnt);
-            }
-        }
-    };
-    if (t < L)
-        horner();
-    // join the full threads 0..L-1: G = sum_u A_u R0^u, u = L-1-t, by pairs with R_l = r^(Q 2^l)
-    const u32 Q = 4u * w;
-    F26 R = f26_from32(P.r0, P.r1, P.r2, P.r3, 0u);
-    {
-        F26 acc = R;  // r^Q by square-and-multiply, Q <= 20 (the same in every thread)
-        F26 base = R;
-        bool have = false;
-        for (u32 e = Q; e; e >>= 1) {
-            if (e & 1u) {
-                acc = have ? f26_mul(acc, base) : base;
-                have = true;
-            }
-            if (e > 1u)
-                base = f26_mul(base, base);
-        }
-        R = acc;
+    horner_pass(b0);
+    for (u32 p = 1; p < npass; p++) {
+        const u32 pb = b0 + p * (u32)NACL_ONE_W;
+        load_pass(pb);
+        xor_pass(pb, key);
+        horner_pass(pb);
     }
+    // 4. join the full threads 0..L-1: G = sum_u A_u R^u, u = L-1-t, by pairs with R_l = r^(Q 2^l)
+    const u32 L = (nblk - 1u) / w;  // the thread holding the last box block
+    const F26 r26 = f26_from32(P.r0, P.r1, P.r2, P.r3, 0u);
+    F26 R = f26_pow(r26, 4u * w);
     const u32 u = L - 1u - t;  // (meaningful for t < L)
     F26 A = f26_from32(P.h0, P.h1, P.h2, P.h3, P.h4);
     if (t < L) {
@@ -3490,14 +3452,16 @@ __global__ __launch_bounds__(NACL_ONE_T) void k_nacl_one(uint8_t *st, uint32_t l
     }
     __syncthreads();
     if (t == L) {
-        if (L > 0) {
+        if (L > 0) {  // H = G r^(n_L) + A_L, n_L = thread L's MAC blocks (>= 1: its last block is not empty)
             F26 G;
 #pragma unroll
             for (int i = 0; i < 5; i++)
                 G.l[i] = s_tree[i];  // u = 0
-            f26_to32(G, P.h0, P.h1, P.h2, P.h3, P.h4);
+            const u32 lo = 64u * b0, hi = len;
+            const u32 nL = (hi - lo + 15u) >> 4;
+            A = f26_add(f26_mul(G, f26_pow(r26, nL)), A);
+            f26_to32(A, P.h0, P.h1, P.h2, P.h3, P.h4);
         }
-        horner();  // continues from G: H = G r^(len_L) + h_L
         u32 tag[4];
         poly_finish(P, tag);
         int rc = 0;
@@ -3507,7 +3471,6 @@ __global__ __launch_bounds__(NACL_ONE_T) void k_nacl_one(uint8_t *st, uint32_t l
             const uint4 tin = *reinterpret_cast<const uint4 *>(in + 16);
             rc = ((tag[0] ^ tin.x) | (tag[1] ^ tin.y) | (tag[2] ^ tin.z) | (tag[3] ^ tin.w)) ? -1 : 0;
         }
-        (void)NP;
         *reinterpret_cast<int *>(st + 56) = rc;
     }
 }
@@ -3843,18 +3806,12 @@ hipError_t czk_open_uniform(const void *in, uint64_t in_stride, void *out, uint6
     return hipGetLastError();
 }
 
-hipError_t czk_box_nacl(const void *in, void *out, uint32_t len, const void *subkey, uint64_t counter, int open,
-                        int *rc, hipStream_t s)
-{
-    hipLaunchKernelGGL(k_box_nacl, dim3(1), dim3(64), 0, s, (const uint8_t *)in, (uint8_t *)out, len,
-                       (const uint8_t *)subkey, counter, open, rc);
-    return hipGetLastError();
-}
+uint32_t czk_nacl_one_limit(void);
 
 hipError_t czk_nacl_one(void *st, uint32_t len, int open, void *subcache, int miss, uint32_t out_off,
                         const uint8_t k[32], const uint8_t n[24], hipStream_t s)
 {
-    if (len < 32u || (len + 63u) / 64u > (uint32_t)(NACL_ONE_T * NACL_ONE_W))
+    if (len < 32u || len > czk_nacl_one_limit() || out_off < 128u + len || out_off > 0xffffffffu - len)
         return hipErrorInvalidValue;
     NaclOneArgs a;
     __builtin_memcpy(a.k, k, 32);
@@ -3867,7 +3824,10 @@ hipError_t czk_nacl_one(void *st, uint32_t len, int open, void *subcache, int mi
     return hipGetLastError();
 }
 
+// one pass of k_nacl_one (80 KiB): the size up to which one launch beats the segment kernels
 uint32_t czk_nacl_one_max(void) { return (uint32_t)(NACL_ONE_T * NACL_ONE_W * 64); }
+// the largest box k_nacl_one takes (jnacl's byte[] bound; 64 * block index and out_off + len fit u32)
+uint32_t czk_nacl_one_limit(void) { return 0x7fffff00u; }
 
 hipError_t czk_subkeys(const void *precom, void *out, uint32_t nkeys, const uint8_t prefix[16], hipStream_t s)
 {

@@ -100,7 +100,7 @@ public:
         for (uint32_t i = 0; i < count; i++)
             if (len[i] > (uint32_t)CZ_MESSAGE_MAX)
                 return fail(CZ_EMSGSIZE, "encode_batch: frame %u (%u bytes) exceeds CZ_MESSAGE_MAX", i, len[i]);
-        if (count == 1 && (uint64_t)len[0] + 33 <= czk_nacl_one_max())
+        if (count == 1 && (uint64_t)len[0] + 33 <= nacl_one_bytes())
             return seal_one(h_in + in_off[0], len[0], msg_flags ? msg_flags[0] : 0u, h_out + out_off[0]);
         // device layout: 16-byte aligned frames, packed; segments of batch_seg_blocks blocks
         std::vector<cz_frame_desc> d(count);
@@ -177,7 +177,7 @@ public:
             return CZ_OK;
         if (!h_in || !in_off || !size || !h_out || !out_off)
             return fail(CZ_EINVAL, "decode_batch: null pointer");
-        if (count == 1 && size[0] <= czk_nacl_one_max())
+        if (count == 1 && size[0] <= nacl_one_bytes())
             return open_one(h_in + in_off[0], size[0], h_out + out_off[0], msg_flags, failed, event);
         std::vector<cz_frame_desc> d(count);
         uint64_t ib = 0, ob = 0, tb = 0, longest = 0;

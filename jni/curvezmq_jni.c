@@ -71,9 +71,21 @@ static void crit_release(JNIEnv *env, crit_arg *v, int n)
 
 #define U8(i) ((uint8_t *)v[i].p)
 
+/* The library creates a thread's single-shot context (HIP stream, device buffers, pinned staging)
+ * on its first call.  Do that before the first pin of each thread, so HIP runtime initialisation
+ * never runs inside a critical region (the GC is locked out while arrays are pinned).  A failure
+ * (no GPU) is left to the call itself, which then returns -1. */
+static _Thread_local int t_warm;
+
+static void warm_thread(void)
+{
+    if (!t_warm && cz_nacl_thread_init() == CZ_OK)
+        t_warm = 1;
+}
+
 /* ---- com.neilalexander.jnacl.crypto.curve25519xsalsa20poly1305 ------------------------------- */
 
-/* Curve.java:129-137 -> crypto_box_afternm(c, m, mlen, n, k): c = box of m (m[0:32] zero) */
+/* Curve.java:129-137 -> crypto_box_afternm(c, m, mlen, n, k): c = NaCl's box of m (any m[0:32]) */
 JNIEXPORT jint JNICALL Java_com_neilalexander_jnacl_crypto_curve25519xsalsa20poly1305_crypto_1box_1afternm(
     JNIEnv *env, jclass cls, jbyteArray c, jbyteArray m, jint mlen, jbyteArray n, jbyteArray k)
 {
@@ -81,6 +93,7 @@ JNIEXPORT jint JNICALL Java_com_neilalexander_jnacl_crypto_curve25519xsalsa20pol
     if (mlen < 32)
         return -1;
     crit_arg v[4] = {{c, mlen, 1, NULL}, {m, mlen, 0, NULL}, {n, 24, 0, NULL}, {k, 32, 0, NULL}};
+    warm_thread();
     if (crit_acquire(env, v, 4))
         return -1;
     const int rc = cz_box_afternm(U8(0), U8(1), (uint64_t)mlen, U8(2), U8(3));
@@ -96,6 +109,7 @@ JNIEXPORT jint JNICALL Java_com_neilalexander_jnacl_crypto_curve25519xsalsa20pol
     if (clen < 32)
         return -1;
     crit_arg v[4] = {{m, clen, 1, NULL}, {c, clen, 0, NULL}, {n, 24, 0, NULL}, {k, 32, 0, NULL}};
+    warm_thread();
     if (crit_acquire(env, v, 4))
         return -1;
     const int rc = cz_box_open_afternm(U8(0), U8(1), (uint64_t)clen, U8(2), U8(3));
@@ -109,6 +123,7 @@ JNIEXPORT jint JNICALL Java_com_neilalexander_jnacl_crypto_curve25519xsalsa20pol
 {
     (void)cls;
     crit_arg v[3] = {{k, 32, 1, NULL}, {pk, 32, 0, NULL}, {sk, 32, 0, NULL}};
+    warm_thread();
     if (crit_acquire(env, v, 3))
         return -1;
     const int rc = cz_box_beforenm(U8(0), U8(1), U8(2));
@@ -124,6 +139,7 @@ JNIEXPORT jint JNICALL Java_com_neilalexander_jnacl_crypto_curve25519xsalsa20pol
     if (mlen < 32)
         return -1;
     crit_arg v[5] = {{c, mlen, 1, NULL}, {m, mlen, 0, NULL}, {n, 24, 0, NULL}, {pk, 32, 0, NULL}, {sk, 32, 0, NULL}};
+    warm_thread();
     if (crit_acquire(env, v, 5))
         return -1;
     const int rc = cz_box(U8(0), U8(1), (uint64_t)mlen, U8(2), U8(3), U8(4));
@@ -139,6 +155,7 @@ JNIEXPORT jint JNICALL Java_com_neilalexander_jnacl_crypto_curve25519xsalsa20pol
     if (clen < 32)
         return -1;
     crit_arg v[5] = {{m, clen, 1, NULL}, {c, clen, 0, NULL}, {n, 24, 0, NULL}, {pk, 32, 0, NULL}, {sk, 32, 0, NULL}};
+    warm_thread();
     if (crit_acquire(env, v, 5))
         return -1;
     const int rc = cz_box_open(U8(0), U8(1), (uint64_t)clen, U8(2), U8(3), U8(4));
@@ -152,6 +169,7 @@ JNIEXPORT jint JNICALL Java_com_neilalexander_jnacl_crypto_curve25519xsalsa20pol
 {
     (void)cls;
     crit_arg v[2] = {{pk, 32, 1, NULL}, {sk, 32, 1, NULL}};
+    warm_thread();
     if (crit_acquire(env, v, 2))
         return -1;
     const int rc = cz_box_keypair(U8(0), U8(1));
@@ -168,6 +186,7 @@ JNIEXPORT jint JNICALL Java_com_neilalexander_jnacl_crypto_xsalsa20poly1305_cryp
     if (mlen < 32)
         return -1;
     crit_arg v[4] = {{c, mlen, 1, NULL}, {m, mlen, 0, NULL}, {n, 24, 0, NULL}, {k, 32, 0, NULL}};
+    warm_thread();
     if (crit_acquire(env, v, 4))
         return -1;
     const int rc = cz_secretbox(U8(0), U8(1), (uint64_t)mlen, U8(2), U8(3));
@@ -182,6 +201,7 @@ JNIEXPORT jint JNICALL Java_com_neilalexander_jnacl_crypto_xsalsa20poly1305_cryp
     if (clen < 32)
         return -1;
     crit_arg v[4] = {{m, clen, 1, NULL}, {c, clen, 0, NULL}, {n, 24, 0, NULL}, {k, 32, 0, NULL}};
+    warm_thread();
     if (crit_acquire(env, v, 4))
         return -1;
     const int rc = cz_secretbox_open(U8(0), U8(1), (uint64_t)clen, U8(2), U8(3));
@@ -190,6 +210,17 @@ JNIEXPORT jint JNICALL Java_com_neilalexander_jnacl_crypto_xsalsa20poly1305_cryp
 }
 
 /* ---- direct ByteBuffers ----------------------------------------------------------------------- */
+
+/* bytes a uniform batch touches: (count - 1) * stride + last; -1 (never a valid need) on overflow */
+static jlong uniform_need(jint count, jlong stride, jlong last)
+{
+    jlong v;
+    if (count <= 0)
+        return 0;
+    if (__builtin_mul_overflow((jlong)(count - 1), stride, &v) || __builtin_add_overflow(v, last, &v))
+        return -1;
+    return v;
+}
 
 /* address of a direct buffer holding at least `need` bytes; NULL if null, not direct, or short */
 static void *direct(JNIEnv *env, jobject buf, jlong need)
@@ -278,8 +309,11 @@ JNIEXPORT jint JNICALL Java_zmq_io_mechanism_curve_GpuCurveBatch_sealUniform(
     if (count == 0)
         return CZ_OK;
     const jlong olen = (jlong)len + CZ_MESSAGE_OVERHEAD;
-    const jlong in_need = count > 1 ? (jlong)(count - 1) * inStride + len : len;
-    const jlong out_need = count > 1 ? (jlong)count * outStride : olen;
+    /* whole output slots: count * outStride (one frame: the body) */
+    const jlong in_need = count > 1 ? uniform_need(count, inStride, len) : len;
+    const jlong out_need = count > 1 ? uniform_need(count, outStride, outStride) : olen;
+    if (in_need < 0 || out_need < 0)
+        return CZ_EINVAL;
     void *pi = direct(env, in, in_need), *po = direct(env, out, out_need);
     const void *pf = flags ? direct(env, flags, count) : NULL;
     if (!pi || !po || (flags && !pf))
@@ -298,8 +332,10 @@ JNIEXPORT jint JNICALL Java_zmq_io_mechanism_curve_GpuCurveBatch_openUniform(
     if (count == 0)
         return CZ_OK;
     const jlong olen = (jlong)size - CZ_MESSAGE_OVERHEAD;
-    const jlong in_need = count > 1 ? (jlong)(count - 1) * inStride + size : size;
-    const jlong out_need = count > 1 ? (jlong)count * outStride : olen;
+    const jlong in_need = count > 1 ? uniform_need(count, inStride, size) : size;
+    const jlong out_need = count > 1 ? uniform_need(count, outStride, outStride) : olen;
+    if (in_need < 0 || out_need < 0)
+        return CZ_EINVAL;
     void *pi = direct(env, in, in_need), *po = direct(env, out, out_need), *ps = direct(env, status, 2 * (jlong)count);
     if (!pi || !po || !ps)
         return CZ_EINVAL;
@@ -307,7 +343,10 @@ JNIEXPORT jint JNICALL Java_zmq_io_mechanism_curve_GpuCurveBatch_openUniform(
                                (uint64_t)outStride, (uint64_t)floor0, check ? 1 : 0, (uint16_t *)ps, (uint32_t)chunk);
 }
 
-/* pinned host memory as a direct ByteBuffer (the pinned MsgAllocator, zmq/msg/MsgAllocator.java:5-8) */
+/* pinned host memory as a direct ByteBuffer (the pinned MsgAllocator, zmq/msg/MsgAllocator.java:5-8);
+ * hostFree releases it: the library frees only base addresses hostAlloc returned (a slice, a
+ * msgAlloc view, ByteBuffer.allocateDirect memory or a second free is refused), and the buffer
+ * must not be used afterwards */
 JNIEXPORT jobject JNICALL Java_zmq_io_mechanism_curve_GpuCurveBatch_hostAlloc(JNIEnv *env, jclass cls, jlong bytes)
 {
     (void)cls;
@@ -393,7 +432,9 @@ JNIEXPORT jobject JNICALL Java_zmq_io_GpuCurveEngine_wireOut(JNIEnv *env, jclass
     return wrap(env, w, len);
 }
 
-/* the same stream as gather-write pieces (SocketChannel.write(ByteBuffer[]), StreamEngine.java:509-535) */
+/* the same stream as gather-write pieces (SocketChannel.write(ByteBuffer[]), StreamEngine.java:509-535).
+ * NULL with the JVM's exception pending when an allocation fails; each piece's local reference is
+ * deleted once it is stored, so a stream of many pieces stays within the local-reference capacity. */
 JNIEXPORT jobjectArray JNICALL Java_zmq_io_GpuCurveEngine_wireIov(JNIEnv *env, jclass cls, jlong e, jint conn)
 {
     (void)cls;
@@ -406,9 +447,24 @@ JNIEXPORT jobjectArray JNICALL Java_zmq_io_GpuCurveEngine_wireIov(JNIEnv *env, j
     jobjectArray out = NULL;
     if (cz_engine_wire_iov(ENG(e), conn, iov, n, &n) == CZ_OK) {
         jclass bb = (*env)->FindClass(env, "java/nio/ByteBuffer");
-        out = bb ? (*env)->NewObjectArray(env, (jsize)n, bb, NULL) : NULL;
-        for (uint32_t i = 0; out && i < n; i++)
-            (*env)->SetObjectArrayElement(env, out, (jsize)i, wrap(env, iov[i].base, iov[i].len));
+        if (bb && !(*env)->ExceptionCheck(env)) {
+            out = (*env)->NewObjectArray(env, (jsize)n, bb, NULL);
+            (*env)->DeleteLocalRef(env, bb);
+            for (uint32_t i = 0; out && i < n; i++) {
+                jobject piece = wrap(env, iov[i].base, iov[i].len);
+                if (!piece || (*env)->ExceptionCheck(env)) {
+                    (*env)->DeleteLocalRef(env, out);
+                    out = NULL;
+                    break;
+                }
+                (*env)->SetObjectArrayElement(env, out, (jsize)i, piece);
+                (*env)->DeleteLocalRef(env, piece);
+                if ((*env)->ExceptionCheck(env)) {
+                    (*env)->DeleteLocalRef(env, out);
+                    out = NULL;
+                }
+            }
+        }
     }
     free(iov);
     return out;

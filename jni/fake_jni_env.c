@@ -23,6 +23,10 @@ struct _jobject {
 };
 
 static int g_copy_mode, g_fail_pin_at = -1, g_pin_count, g_outstanding, g_calls_in_critical;
+/* local references the shim created (NewDirectByteBuffer, NewObjectArray, FindClass results handed
+ * out) and not deleted, their high-water mark, and an injected allocation failure: the n-th
+ * NewDirectByteBuffer returns NULL with an OutOfMemoryError pending, as a JVM does */
+static int g_live_refs, g_max_live_refs, g_fail_new_at = -1, g_new_count, g_exception;
 static int g_modes[64], g_nmodes;
 
 static size_t elem_size(jobject o) { return o->kind == K_INTS ? 4 : 1; }
@@ -33,7 +37,28 @@ static jclass f_FindClass(JNIEnv *env, const char *name)
     static struct _jobject cls = {K_CLASS, 0, NULL, 0, 0, 0, 0, NULL, NULL};
     if (g_outstanding)
         g_calls_in_critical++;
-    return strcmp(name, "java/nio/ByteBuffer") == 0 ? &cls : NULL;
+    if (strcmp(name, "java/nio/ByteBuffer") != 0) {
+        g_exception = 1; /* NoClassDefFoundError */
+        return NULL;
+    }
+    if (++g_live_refs > g_max_live_refs)
+        g_max_live_refs = g_live_refs;
+    return &cls;
+}
+
+static void f_DeleteLocalRef(JNIEnv *env, jobject o)
+{
+    (void)env;
+    if (o)
+        g_live_refs--;
+}
+
+static jboolean f_ExceptionCheck(JNIEnv *env)
+{
+    (void)env;
+    if (g_outstanding)
+        g_calls_in_critical++;
+    return (jboolean)(g_exception != 0);
 }
 
 static jsize f_GetArrayLength(JNIEnv *env, jarray a)
@@ -48,6 +73,8 @@ static jobjectArray f_NewObjectArray(JNIEnv *env, jsize len, jclass cls, jobject
 {
     (void)env, (void)cls, (void)init;
     jobject o = (jobject)calloc(1, sizeof *o);
+    if (++g_live_refs > g_max_live_refs)
+        g_max_live_refs = g_live_refs;
     o->kind = K_OBJARRAY;
     o->len = len;
     o->elems = (jobject *)calloc(len ? (size_t)len : 1, sizeof(jobject));
@@ -106,6 +133,12 @@ static void f_ReleasePrimitiveArrayCritical(JNIEnv *env, jarray a, void *p, jint
 static jobject f_NewDirectByteBuffer(JNIEnv *env, void *p, jlong cap)
 {
     (void)env;
+    if (g_new_count++ == g_fail_new_at) {
+        g_exception = 1;
+        return NULL;
+    }
+    if (++g_live_refs > g_max_live_refs)
+        g_max_live_refs = g_live_refs;
     jobject o = (jobject)calloc(1, sizeof *o);
     o->kind = K_DIRECT;
     o->data = p;
@@ -131,6 +164,8 @@ static const struct JNINativeInterface_ *g_env = &g_table;
 JNIEnv *fake_env(void)
 {
     g_table.FindClass = f_FindClass;
+    g_table.DeleteLocalRef = f_DeleteLocalRef;
+    g_table.ExceptionCheck = f_ExceptionCheck;
     g_table.GetArrayLength = f_GetArrayLength;
     g_table.NewObjectArray = f_NewObjectArray;
     g_table.SetObjectArrayElement = f_SetObjectArrayElement;
@@ -161,6 +196,11 @@ jobject fake_heap_buffer(void) { return new_obj(K_DIRECT, NULL, 0, 0); } /* a no
 void fake_set_copy_mode(int on) { g_copy_mode = on; }
 void fake_fail_pin_at(int n) { g_fail_pin_at = n, g_pin_count = 0; }
 void fake_reset_log(void) { g_nmodes = 0, g_calls_in_critical = 0, g_pin_count = 0, g_fail_pin_at = -1; }
+void fake_reset_refs(void) { g_live_refs = g_max_live_refs = 0, g_new_count = 0, g_fail_new_at = -1, g_exception = 0; }
+void fake_fail_new_at(int n) { g_fail_new_at = n, g_new_count = 0; }
+int fake_live_refs(void) { return g_live_refs; }
+int fake_max_live_refs(void) { return g_max_live_refs; }
+int fake_exception(void) { return g_exception; }
 int fake_outstanding(void) { return g_outstanding; }
 int fake_calls_in_critical(void) { return g_calls_in_critical; }
 int fake_nmodes(void) { return g_nmodes; }

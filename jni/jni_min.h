@@ -45,7 +45,9 @@ struct JNINativeInterface_ {
     jclass (*FindClass)(JNIEnv *env, const char *name);                                       /* 6 */
     CZ_JNI_PAD(7, 14);
     jint (*ThrowNew)(JNIEnv *env, jclass cls, const char *msg);                               /* 14 */
-    CZ_JNI_PAD(15, 171);
+    CZ_JNI_PAD(15, 23);
+    void (*DeleteLocalRef)(JNIEnv *env, jobject obj);                                         /* 23 */
+    CZ_JNI_PAD(24, 171);
     jsize (*GetArrayLength)(JNIEnv *env, jarray array);                                       /* 171 */
     jobjectArray (*NewObjectArray)(JNIEnv *env, jsize len, jclass cls, jobject init);        /* 172 */
     void *GetObjectArrayElement;                                                              /* 173 */
@@ -55,7 +57,8 @@ struct JNINativeInterface_ {
     CZ_JNI_PAD(212, 222);
     void *(*GetPrimitiveArrayCritical)(JNIEnv *env, jarray array, jboolean *isCopy);          /* 222 */
     void (*ReleasePrimitiveArrayCritical)(JNIEnv *env, jarray array, void *carray, jint mode); /* 223 */
-    CZ_JNI_PAD(224, 229);
+    CZ_JNI_PAD(224, 228);
+    jboolean (*ExceptionCheck)(JNIEnv *env);                                                  /* 228 */
     jobject (*NewDirectByteBuffer)(JNIEnv *env, void *address, jlong capacity);              /* 229 */
     void *(*GetDirectBufferAddress)(JNIEnv *env, jobject buf);                                /* 230 */
     jlong (*GetDirectBufferCapacity)(JNIEnv *env, jobject buf);                               /* 231 */
@@ -65,12 +68,14 @@ struct JNINativeInterface_ {
 #define CZ_JNI_SLOT(f, i) _Static_assert(offsetof(struct JNINativeInterface_, f) == (i) * sizeof(void *), #f)
 CZ_JNI_SLOT(FindClass, 6);
 CZ_JNI_SLOT(ThrowNew, 14);
+CZ_JNI_SLOT(DeleteLocalRef, 23);
 CZ_JNI_SLOT(GetArrayLength, 171);
 CZ_JNI_SLOT(NewObjectArray, 172);
 CZ_JNI_SLOT(SetObjectArrayElement, 174);
 CZ_JNI_SLOT(SetIntArrayRegion, 211);
 CZ_JNI_SLOT(GetPrimitiveArrayCritical, 222);
 CZ_JNI_SLOT(ReleasePrimitiveArrayCritical, 223);
+CZ_JNI_SLOT(ExceptionCheck, 228);
 CZ_JNI_SLOT(NewDirectByteBuffer, 229);
 CZ_JNI_SLOT(GetDirectBufferAddress, 230);
 CZ_JNI_SLOT(GetDirectBufferCapacity, 231);

@@ -162,6 +162,28 @@ def main():
         bx.append({"key": key.hex(), "nonce": n24.hex(), "m_seed": 0x9000 + i, "n": n, "c": c.hex()})
     out["box_afternm"] = bx
 
+    # crypto_box_afternm of an m whose first 32 bytes are NOT zero.  NaCl (and libsodium, and jnacl's
+    # port of it) accept it: c = keystream ^ m over all mlen bytes, Poly1305 keyed with
+    # c[0:32] = keystream[0:32] ^ m[0:32], tag at c[16:32], c[0:16] = 0.  JeroMQ's public Curve.box
+    # (Curve.java:184-193) hands such an m to jnacl.  The open (keyed with the keystream alone) then
+    # fails on these boxes, as in NaCl.  Sizes straddle the one-pass / segmented edge (80 KiB).
+    bp = []
+    for i, mlen in enumerate([32, 33, 133, 4129, 81953]):
+        key = splitmix_bytes(32, 0x7100 + i)
+        n24 = splitmix_bytes(24, 0x8100 + i)
+        m = splitmix_bytes(mlen, 0x9100 + i)
+        assert any(m[:32])
+        rc, c = box_afternm(m, n24, key)
+        assert rc == 0 and c[:16] == bytes(16)
+        rc0, c0 = box_afternm(bytes(32) + m[32:], n24, key)
+        assert rc0 == 0 and c0[32:] == c[32:] and c0[16:32] != c[16:32]
+        rco, _ = box_open_afternm(c, n24, key)
+        assert rco == -1
+        bp.append({"key": key.hex(), "nonce": n24.hex(), "m_seed": 0x9100 + i, "mlen": mlen,
+                   "tag": c[16:32].hex(), "sha256": hashlib.sha256(c).hexdigest(),
+                   **({"c": c.hex()} if mlen <= 4129 else {})})
+    out["box_afternm_prefix"] = bp
+
     # CurveZMQ MESSAGE bodies under the RFC test keys (SURVEY.md 8(c) case list)
     sizes = [0, 1, 15, 16, 17, 31, 32, 33, 47, 63, 64, 65, 100, 255, 256, 4096, 65536]
     counters = [2, 3, (1 << 32) - 1, 1 << 32, (1 << 63) - 1]

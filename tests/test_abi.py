@@ -91,6 +91,16 @@ def test_no_cpu_fallback_without_gpu(lib):
     assert not lib.cz_mech_create(0, bytes(32), 3, 1, 0)
 
 
+def test_host_free_refuses_foreign_pointers(lib):
+    """cz_host_free releases only live cz_host_alloc base addresses: a foreign or interior pointer
+    is CZ_EINVAL and never reaches hipHostFree (hostFree of any direct ByteBuffer)."""
+    from jeromq_amd import _lib
+    buf = ctypes.create_string_buffer(64)
+    assert lib.cz_host_free(ctypes.addressof(buf)) == _lib.CZ_EINVAL
+    assert lib.cz_host_free(ctypes.addressof(buf) + 16) == _lib.CZ_EINVAL
+    assert lib.cz_host_free(None) == _lib.CZ_OK
+
+
 def test_plan_order_host_logic(lib):
     from jeromq_amd.batch import plan_order
     d = np.zeros(6, dtype=DESC_DTYPE)

@@ -385,20 +385,12 @@ def test_nacl_box_afternm_golden(L, torch_dev):
 
 
 def test_nacl_one_launch_contract_and_subkey_cache(L, torch_dev):
-    """The one-launch drop-in (k_nacl_one): NaCl's ZEROBYTES contract -- a seal of an m whose first
-    32 bytes are not zero returns -1 (NaCl would key the MAC with them; the device path does not),
-    output untouched; the per-thread subkey cache -- 12 keys cycled through the 8-entry cache,
-    the same key under two nonce prefixes (client / server direction), cz_nacl_forget in between --
-    never serves a stale subkey: every box against the oracle."""
+    """The one-launch drop-in (k_nacl_one): the per-thread subkey cache -- 12 keys cycled through the
+    8-entry cache, the same key under two nonce prefixes (client / server direction),
+    cz_nacl_forget in between -- never serves a stale subkey: every box against the oracle."""
     from cz_testlib import or_box_afternm
     lib = L.lib()
     rng = np.random.default_rng(5)
-    m = bytearray(32 + 100)
-    m[32:] = rng.integers(0, 256, 100, dtype=np.uint8).tobytes()
-    m[5] = 1
-    c = ctypes.create_string_buffer(b"\x5a" * len(m), len(m))
-    assert lib.cz_box_afternm(c, bytes(m), len(m), bytes(24), bytes(32)) == -1
-    assert c.raw == b"\x5a" * len(m)
     keys = [rng.integers(0, 256, 32, dtype=np.uint8).tobytes() for _ in range(12)]
     for rnd in range(3):
         for i, key in enumerate(keys):
@@ -414,6 +406,67 @@ def test_nacl_one_launch_contract_and_subkey_cache(L, torch_dev):
                 assert lib.cz_box_open_afternm(back, want, mlen, n24, key) == 0 and back.raw == mm
         if rnd == 1:
             assert lib.cz_nacl_forget() == 0
+
+
+@pytest.mark.parametrize("v", G["box_afternm_prefix"], ids=lambda v: f"mlen{v['mlen']}")
+def test_nacl_box_nonzero_prefix_golden(L, torch_dev, v):
+    """NaCl's crypto_box_afternm for EVERY m (Curve.box, Curve.java:184-193, hands jnacl any m): an m
+    whose first 32 bytes are not zero seals with rc 0, the ciphertext of its zero-prefixed twin and
+    the tag of a MAC keyed with c[0:32] = keystream ^ m[0:32] -- libsodium's box, byte for byte,
+    through cz_box_afternm and cz_secretbox (81953 bytes: past the one-pass 80 KiB, several passes of
+    k_nacl_one).  The open of such a box fails as in NaCl (its MAC key is the keystream alone), and
+    leaves the output untouched."""
+    import hashlib
+    lib = L.lib()
+    key, n24 = bytes.fromhex(v["key"]), bytes.fromhex(v["nonce"])
+    m = splitmix_bytes(v["mlen"], v["m_seed"])
+    for fn in (lib.cz_box_afternm, lib.cz_secretbox):
+        c = ctypes.create_string_buffer(b"\x5a" * len(m), len(m))
+        assert fn(c, m, len(m), n24, key) == 0
+        assert c.raw[:16] == bytes(16) and c.raw[16:32].hex() == v["tag"]
+        assert hashlib.sha256(c.raw).hexdigest() == v["sha256"]
+        if "c" in v:
+            assert c.raw.hex() == v["c"]
+    out = ctypes.create_string_buffer(b"\x33" * len(m), len(m))
+    assert lib.cz_box_open_afternm(out, c.raw, len(m), n24, key) == -1
+    assert out.raw == b"\x33" * len(m)
+
+
+@pytest.mark.parametrize("one_max", [80 << 10, 1 << 22])
+def test_nacl_one_multi_pass_against_oracle(L, torch_dev, one_max):
+    """k_nacl_one past one pass (boxes > 80 KiB walk several passes of 5 blocks per thread, the MAC
+    joined as G r^(n_L) + A_L): random m (zero and non-zero m[0:32]) at sizes around the pass and
+    thread edges, against the oracle; with cz_tune("nacl_one_max") at 4 MiB the zero-prefix seals
+    and every open take it too, otherwise the segment kernels -- both must agree with NaCl."""
+    from cz_testlib import or_box_afternm, or_box_open_afternm
+    lib = L.lib()
+    old = lib.cz_tune(b"nacl_one_max", one_max)
+    try:
+        rng = np.random.default_rng(one_max & 0xffff)
+        key = rng.integers(0, 256, 32, dtype=np.uint8).tobytes()
+        sizes = [81920, 81921, 81953, 81920 + 64 * 256, 163840, 163841 + 15, 409600 + 7, 1 << 20, 3 * (1 << 20) + 33]
+        for j, mlen in enumerate(sizes):
+            n24 = rng.integers(0, 256, 24, dtype=np.uint8).tobytes()
+            body = rng.integers(0, 256, mlen - 32, dtype=np.uint8).tobytes()
+            for m in (bytes(32) + body, rng.integers(0, 256, 32, dtype=np.uint8).tobytes() + body):
+                rc, want = or_box_afternm(m, n24, key)
+                assert rc == 0
+                c = ctypes.create_string_buffer(mlen)
+                assert lib.cz_box_afternm(c, m, mlen, n24, key) == 0, (mlen, L.last_error())
+                assert c.raw == want, (mlen, m[:32] == bytes(32))
+            # open the zero-prefix box; tamper the last byte
+            _, want = or_box_afternm(bytes(32) + body, n24, key)
+            back = ctypes.create_string_buffer(mlen)
+            assert lib.cz_box_open_afternm(back, want, mlen, n24, key) == 0
+            assert back.raw == bytes(32) + body
+            bad = bytearray(want)
+            bad[-1] ^= 1
+            assert or_box_open_afternm(bytes(bad), n24, key)[0] == -1
+            back2 = ctypes.create_string_buffer(b"\x11" * mlen, mlen)
+            assert lib.cz_box_open_afternm(back2, bytes(bad), mlen, n24, key) == -1
+            assert back2.raw == b"\x11" * mlen
+    finally:
+        lib.cz_tune(b"nacl_one_max", old)
 
 
 def test_nacl_single_shot_multi_lane(L, torch_dev):
@@ -516,22 +569,29 @@ def test_mechanism_batches(L, torch_dev):
 
 
 def test_mechanism_one_launch_and_segmented_paths(L, torch_dev):
-    """encode / decode of one MESSAGE up to 80 KiB run in one launch (k_nacl_one) with the
-    mechanism's own subkeys; longer ones and batches run the segment kernels with the segment length
-    scaled to the batch.  Bodies against the oracle on both sides of the 80 KiB edge, a ragged batch
-    of long and short frames, and the header rejections of the one-launch path (short body,
-    wrong command, replay) against the reference's events."""
+    """encode / decode of one MESSAGE up to 2 MiB (cz_tune "nacl_one_max") run in one launch
+    (k_nacl_one, one pass up to 80 KiB, several above) with the mechanism's own subkeys; longer ones
+    and batches run the segment kernels with the segment length scaled to the batch.  Bodies against
+    the oracle on both sides of the one-pass 80 KiB edge and of the one-launch edge (the default and
+    one moved to 80 KiB), a ragged batch of long and short frames, and the header rejections of the
+    one-launch path (short body, wrong command, replay) against the reference's events."""
     from jeromq_amd.mechanism import CurveClientMechanism, CurveServerMechanism, Msg
     cli = CurveClientMechanism(PRECOM)
     srv = CurveServerMechanism(PRECOM)
     nonce = 3
-    for n in (81919 - 33, 81920 - 33, 81921 - 33, 200000):
-        p = splitmix_bytes(n, n)
-        enc = cli.encode(Msg(p, 1))
-        assert enc.data == or_curve_encode(p, 1, nonce, 0, PRECOM), n
-        dec = srv.decode(enc)
-        assert dec is not None and dec.data == p and dec.flags == 1, n
-        nonce += 1
+    lib = L.lib()
+    for knob in (2 << 20, 80 << 10):
+        old = lib.cz_tune(b"nacl_one_max", knob)
+        try:
+            for n in (81919 - 33, 81920 - 33, 81921 - 33, 200000, (2 << 20) - 33, (2 << 20) - 32):
+                p = splitmix_bytes(n, n)
+                enc = cli.encode(Msg(p, 1))
+                assert enc.data == or_curve_encode(p, 1, nonce, 0, PRECOM), (knob, n)
+                dec = srv.decode(enc)
+                assert dec is not None and dec.data == p and dec.flags == 1, (knob, n)
+                nonce += 1
+        finally:
+            lib.cz_tune(b"nacl_one_max", old)
     msgs = [Msg(splitmix_bytes(n, 7 * n + 1), n & 3) for n in (100000, 1, 5000, 0, 300000, 64)]
     enc = cli.encodeBatch(msgs)
     for i, (m, e) in enumerate(zip(msgs, enc)):

@@ -61,6 +61,7 @@ def shim(tmp_path_factory):
     for f in ("fake_pins", "fake_releases", "fake_last_mode", "fake_kind", "fake_len", "fake_addr", "fake_cap"):
         getattr(L, f).argtypes = [vp]
     L.fake_elem.argtypes = [vp, i32]
+    L.fake_fail_new_at.argtypes = [i32]
     for n in NATIVES:
         fn = getattr(L, n)
         fn.restype = vp if n.endswith(("hostAlloc", "msgAlloc", "wireOut", "wireIov", "msgIn")) else i32
@@ -207,6 +208,24 @@ def test_batch_and_engine_refuse_bad_buffers(shim):
     assert getattr(L, ENGINE + "flushOut")(L.env, None, ctypes.c_int64(0)) == CZ_EINVAL
 
 
+def test_uniform_strides_that_overflow_are_refused(shim):
+    """count x stride products are checked before the library is entered: a 2^62 stride over 4 frames
+    wraps a signed 64-bit need to 0 (so any buffer would pass) -- refused with CZ_EINVAL, as is a
+    stride whose (count - 1) * stride + len overflows."""
+    L = shim
+    buf = np.zeros(1 << 12, dtype=np.uint8)
+    d = L.fake_direct(buf.ctypes.data, buf.nbytes)
+    su = getattr(L, BATCH + "sealUniform")
+    su.argtypes = [vp, vp, i64, i32, i32, vp, i64, vp, i64, i64, vp, i32]
+    assert su(L.env, None, 1, 4, 100, d, 112, d, 1 << 62, 3, None, 0) == CZ_EINVAL
+    assert su(L.env, None, 1, 4, 100, d, 1 << 62, d, 144, 3, None, 0) == CZ_EINVAL
+    assert su(L.env, None, 1, 3, 100, d, (1 << 62) + 1, d, 144, 3, None, 0) == CZ_EINVAL
+    ou = getattr(L, BATCH + "openUniform")
+    ou.argtypes = [vp, vp, i64, i32, i32, vp, i64, vp, i64, i64, ctypes.c_uint8, vp, i32]
+    assert ou(L.env, None, 1, 4, 133, d, 144, d, 1 << 62, 2, 1, d, 0) == CZ_EINVAL
+    assert ou(L.env, None, 1, 4, 133, d, 1 << 62, d, 112, 2, 1, d, 0) == CZ_EINVAL
+
+
 def _has_gpu():
     try:
         import torch
@@ -241,6 +260,20 @@ def test_jni_seal_open_through_the_shim(shim):
         c.np[60] ^= 1
         assert getattr(L, JNACL + "crypto_1box_1open_1afternm")(L.env, None, back.obj, c.obj, 133, n.obj, k.obj) == -1
         assert L.fake_outstanding() == 0
+        # NaCl for every m: a box whose m[0:32] is not zero seals (rc 0) to libsodium's bytes, through
+        # crypto_box_afternm and crypto_secretbox alike (golden vectors, tests/golden/make_golden.py)
+        from cz_testlib import load_golden
+        for v in load_golden()["box_afternm_prefix"]:
+            if "c" not in v:
+                continue
+            mlen = v["mlen"]
+            for fn in (JNACL + "crypto_1box_1afternm", SECRETBOX + "crypto_1secretbox"):
+                cc = Arr(L, np.full(mlen, 0x5A, np.uint8))
+                mm = Arr(L, _u8(splitmix_bytes(mlen, v["m_seed"])))
+                assert getattr(L, fn)(L.env, None, cc.obj, mm.obj, mlen, Arr(L, _u8(bytes.fromhex(v["nonce"]))).obj,
+                                      Arr(L, _u8(bytes.fromhex(v["key"]))).obj) == 0, (fn, mlen)
+                assert cc.np.tobytes().hex() == v["c"], (fn, mlen)
+        assert L.fake_outstanding() == 0 and L.fake_calls_in_critical() == 0
     finally:
         L.fake_set_copy_mode(0)
 
@@ -310,8 +343,17 @@ def test_jni_batch_and_engine_through_the_shim(shim):
     assert got == want
     wi = getattr(L, ENGINE + "wireIov")
     wi.argtypes = [vp, vp, i64, i32]
+    L.fake_reset_refs()
     arr = wi(L.env, None, e, conn)
     pieces = [L.fake_elem(arr, i) for i in range(L.fake_len(arr))]
     assert b"".join(ctypes.string_at(L.fake_addr(p), L.fake_cap(p)) for p in pieces) == want
+    # each piece's local reference is deleted once stored: only the returned array stays live
+    assert L.fake_live_refs() == 1 and L.fake_max_live_refs() <= 3 and not L.fake_exception()
+    # an allocation that fails (exception pending) ends the call: NULL, no reference left behind
+    L.fake_reset_refs()
+    L.fake_fail_new_at(0)
+    assert not wi(L.env, None, e, conn)
+    assert L.fake_exception() and L.fake_live_refs() == 0
+    L.fake_reset_refs()
     getattr(L, ENGINE + "destroy").argtypes = [vp, vp, i64]
     getattr(L, ENGINE + "destroy")(L.env, None, e)

@@ -52,6 +52,23 @@ def test_box_afternm_roundtrip(v):
     assert or_box_open_afternm(bytes(bad), n24, key)[0] == -1
 
 
+@pytest.mark.parametrize("v", G["box_afternm_prefix"])
+def test_box_afternm_nonzero_prefix(v):
+    """NaCl keys the MAC with c[0:32] = keystream ^ m[0:32]: an m whose first 32 bytes are not zero is
+    sealed (rc 0) with the same ciphertext and a different tag (libsodium fixtures)."""
+    import hashlib
+    key, n24 = bytes.fromhex(v["key"]), bytes.fromhex(v["nonce"])
+    m = splitmix_bytes(v["mlen"], v["m_seed"])
+    rc, c = or_box_afternm(m, n24, key)
+    assert rc == 0 and c[:16] == bytes(16) and c[16:32].hex() == v["tag"]
+    assert hashlib.sha256(c).hexdigest() == v["sha256"]
+    if "c" in v:
+        assert c.hex() == v["c"]
+    rc0, c0 = or_box_afternm(bytes(32) + m[32:], n24, key)
+    assert rc0 == 0 and c0[32:] == c[32:]
+    assert or_box_open_afternm(c, n24, key)[0] == -1  # the open keys the MAC with the keystream
+
+
 def test_box_short_inputs_rejected():
     key, n24 = bytes(32), bytes(24)
     assert or_box_afternm(bytes(31), n24, key)[0] == -1

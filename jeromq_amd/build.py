@@ -21,9 +21,10 @@ from concurrent.futures import ThreadPoolExecutor
 HERE = os.path.dirname(os.path.abspath(__file__))
 ROOT = os.path.dirname(HERE)
 CSRC = os.path.join(HERE, "csrc")
-LIB = os.environ.get("CZ_LIB_OUT", os.path.join(HERE, "libcurvezmq_mi355x.so"))
+PRODUCT_LIB = os.path.join(HERE, "libcurvezmq_mi355x.so")
+LIB = os.environ.get("CZ_LIB_OUT", PRODUCT_LIB)
 SOURCES = ["cz_kernels.hip", "cz_x25519.hip", "cz_host.cpp", "cz_mechanism.cpp", "cz_wire.cpp", "cz_engine.cpp", "cz_handshake.cpp", "cz_curve_hs.cpp"]
-HEADERS = ["cz_device.h", "cz_internal.h", "cz_salsa_lazy.h", "cz_salsa_tail.h", os.path.join("..", "..", "include", "curvezmq_mi355x.h")]
+HEADERS = ["cz_device.h", "cz_diag.h", "cz_internal.h", "cz_salsa_lazy.h", "cz_salsa_tail.h", os.path.join("..", "..", "include", "curvezmq_mi355x.h")]
 ARCH = os.environ.get("CZ_OFFLOAD_ARCH", "gfx950")
 LLVM_BIN = "/opt/rocm/lib/llvm/bin"
 BUNDLE_MAGIC = b"__CLANG_OFFLOAD_BUNDLE__"
@@ -31,6 +32,26 @@ BUNDLE_MAGIC = b"__CLANG_OFFLOAD_BUNDLE__"
 
 class IsaHazardError(RuntimeError):
     pass
+
+
+class ProductFlagsError(ValueError):
+    """Extra compile flags (A/B variants, wrong-output diagnostics) asked for the product library."""
+
+
+def compile_flags(lib, extra_env=None):
+    """hipcc flags for `lib`.  The product library (jeromq_amd/libcurvezmq_mi355x.so, what
+    jeromq_amd._lib loads and the GPU box runs) is built with exactly the committed flags plus
+    -DCZ_PRODUCT_BUILD: CZ_EXTRA_FLAGS is refused for it, so a variable left set on a build box can
+    never ship an A/B variant or a wrong-output diagnostic (cz_diag.h also #errors on one).  A/B
+    builds name another output with CZ_LIB_OUT (tools/build_variant.sh)."""
+    raw = os.environ.get("CZ_EXTRA_FLAGS", "") if extra_env is None else extra_env
+    extra = raw.split()
+    product = os.path.realpath(lib) == os.path.realpath(PRODUCT_LIB)
+    if product and extra:
+        raise ProductFlagsError(f"CZ_EXTRA_FLAGS={raw!r} refused for the product library {PRODUCT_LIB}: "
+                                "A/B builds set CZ_LIB_OUT to another path")
+    common = [f"--offload-arch={ARCH}", "-O3", "-std=c++17", "-fPIC", "-Wall"]
+    return common + (["-DCZ_PRODUCT_BUILD"] if product else extra)
 
 
 def _stale(lib=LIB, sources=SOURCES):
@@ -107,11 +128,11 @@ def build_library(force=False, verbose=True, sources=None, lib=None, src_dir=Non
     sources = list(sources or SOURCES)
     lib = lib or LIB
     src_dir = src_dir or CSRC
+    compile_flags(lib)  # refuse product-library builds with extra flags before anything else
     if not force and src_dir == CSRC and not _stale(lib, sources):
         return lib
     hipcc = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
-    extra = os.environ.get("CZ_EXTRA_FLAGS", "").split()  # A/B experiments only (e.g. -DCZ_SEAL_WAVES_PER_EU=5)
-    common = [f"--offload-arch={arch}" for arch in [ARCH]] + ["-O3", "-std=c++17", "-fPIC", "-Wall"] + extra
+    common = compile_flags(lib)
     objdir = tempfile.mkdtemp(prefix="cz_build_")
     try:
         def compile_one(f):

@@ -117,7 +117,7 @@ __device__ __forceinline__ void rounds12_frame(u32 x[16], const SalsaFrame &f, u
 // the scalar unit and reads uniform words as SGPR operands.  Rounds 3..20 keep most
 // `w ^= R` updates pending and let v_xad_u32 ((a ^ b) + c) and v_bitop3_b32 (a ^ b ^ c)
 // absorb them: 736 VALU instead of 864.  On return word w is x[w] ^ d[w] for the bits of
-// CZ_LAZY_PENDING, x[w] otherwise.  -DCZ_SALSA_EAGER builds the plain rounds (A/B).
+// CZ_LAZY_PENDING, x[w] otherwise.
 // R12: rounds 1-2 already done by the caller (rounds12_frame).
 static_assert(CZ_LAZY_FIRST_ROUND == 3, "rounds_lazy runs rounds 1-2 in C");
 template <bool R12 = false>
@@ -127,38 +127,6 @@ __device__ __forceinline__ void rounds_lazy(u32 x[16], u32 d[16])
         col_round(x);
         row_round(x);
     }
-#ifdef CZ_SALSA_EAGER
-#pragma unroll
-    for (int i = 1; i < 10; i++) {
-        col_round(x);
-        row_round(x);
-    }
-#pragma unroll
-    for (int k = 0; k < 16; k++)
-        d[k] = 0u;
-#elif defined(CZ_SALSA_LAZY_SPLIT)
-    // one asm statement per round (same instructions): independent work can go in between
-    u32 t0, t1, t2, t3;
-#define CZ_LZ_X "+v"(x[0]), "+v"(x[1]), "+v"(x[2]), "+v"(x[3]), "+v"(x[4]), "+v"(x[5]), "+v"(x[6]), "+v"(x[7]), \
-                "+v"(x[8]), "+v"(x[9]), "+v"(x[10]), "+v"(x[11]), "+v"(x[12]), "+v"(x[13]), "+v"(x[14]), "+v"(x[15])
-#define CZ_LZ_T "=&v"(t0), "=&v"(t1), "=&v"(t2), "=&v"(t3)
-#define CZ_LZ_D(M) M(d[0]), M(d[1]), M(d[2]), M(d[3]), M(d[4]), M(d[5]), M(d[6]), M(d[7]), M(d[8]), M(d[9]), \
-                   M(d[10]), M(d[11]), M(d[12]), M(d[13]), M(d[14]), M(d[15])
-#define CZ_LZ_OUT(v) "=&v"(v)
-#define CZ_LZ_IO(v) "+v"(v)
-#define CZ_LZ_R(i) asm(CZ_SALSA_LAZY_ROUND_##i : CZ_LZ_X, CZ_LZ_D(CZ_LZ_IO), CZ_LZ_T)
-    asm(CZ_SALSA_LAZY_ROUND_0 : CZ_LZ_X, CZ_LZ_D(CZ_LZ_OUT), CZ_LZ_T);
-    CZ_LZ_R(1); CZ_LZ_R(2); CZ_LZ_R(3); CZ_LZ_R(4); CZ_LZ_R(5); CZ_LZ_R(6); CZ_LZ_R(7); CZ_LZ_R(8);
-    CZ_LZ_R(9); CZ_LZ_R(10); CZ_LZ_R(11); CZ_LZ_R(12); CZ_LZ_R(13); CZ_LZ_R(14); CZ_LZ_R(15); CZ_LZ_R(16);
-    CZ_LZ_R(17);
-    static_assert(CZ_LAZY_FIRST_ROUND + 17 == 20, "per-round list covers rounds 3..20");
-#undef CZ_LZ_R
-#undef CZ_LZ_IO
-#undef CZ_LZ_OUT
-#undef CZ_LZ_D
-#undef CZ_LZ_T
-#undef CZ_LZ_X
-#else
     u32 t0, t1, t2, t3;
     asm(CZ_SALSA_LAZY_ASM
         : "+v"(x[0]), "+v"(x[1]), "+v"(x[2]), "+v"(x[3]), "+v"(x[4]), "+v"(x[5]), "+v"(x[6]), "+v"(x[7]),
@@ -166,17 +134,9 @@ __device__ __forceinline__ void rounds_lazy(u32 x[16], u32 d[16])
           "=&v"(d[0]), "=&v"(d[1]), "=&v"(d[2]), "=&v"(d[3]), "=&v"(d[4]), "=&v"(d[5]), "=&v"(d[6]), "=&v"(d[7]),
           "=&v"(d[8]), "=&v"(d[9]), "=&v"(d[10]), "=&v"(d[11]), "=&v"(d[12]), "=&v"(d[13]), "=&v"(d[14]),
           "=&v"(d[15]), "=&v"(t0), "=&v"(t1), "=&v"(t2), "=&v"(t3));
-#endif
 }
 
-__device__ __forceinline__ constexpr bool lazy_pending(int k)
-{
-#ifdef CZ_SALSA_EAGER
-    return k < 0;
-#else
-    return (CZ_LAZY_PENDING >> k) & 1u;
-#endif
-}
+__device__ __forceinline__ constexpr bool lazy_pending(int k) { return (CZ_LAZY_PENDING >> k) & 1u; }
 
 // The 20 rounds with plain xors (compiler-scheduled).
 __device__ __forceinline__ void rounds_eager(u32 x[16])
@@ -231,13 +191,9 @@ __device__ __forceinline__ void salsa20_block_frame(u32 x[16], const SalsaFrame 
 // The last block of a box that uses at most 16 of its bytes (a 100-byte MESSAGE: 133-byte box, 5
 // bytes of block 2): keystream words 0..3 only.  Rounds 3..20 run the tail schedule
 // (cz_salsa_tail.h: the instructions words 0..3 depend on, 692 instead of 736) and the
-// feed-forward covers 4 words; x[4..15] are left unspecified.  The eager path computes the full
-// block and lets the compiler drop what words 0..3 do not need.
+// feed-forward covers 4 words; x[4..15] are left unspecified.
 __device__ __forceinline__ void tail_lazy(u32 x[16], u32 d[16])
 {
-#ifdef CZ_SALSA_EAGER
-    rounds_lazy<true>(x, d);
-#else
     u32 t0, t1, t2, t3;
     asm(CZ_SALSA_TAIL_ASM
         : "+v"(x[0]), "+v"(x[1]), "+v"(x[2]), "+v"(x[3]), "+v"(x[4]), "+v"(x[5]), "+v"(x[6]), "+v"(x[7]),
@@ -245,7 +201,6 @@ __device__ __forceinline__ void tail_lazy(u32 x[16], u32 d[16])
           "=&v"(d[0]), "=&v"(d[1]), "=&v"(d[2]), "=&v"(d[3]), "=&v"(d[4]), "=&v"(d[5]), "=&v"(d[6]), "=&v"(d[7]),
           "=&v"(d[8]), "=&v"(d[9]), "=&v"(d[10]), "=&v"(d[11]), "=&v"(d[12]), "=&v"(d[13]), "=&v"(d[14]),
           "=&v"(d[15]), "=&v"(t0), "=&v"(t1), "=&v"(t2), "=&v"(t3));
-#endif
 }
 static_assert(CZ_SALSA_TAIL_WORDS == 4, "tail blocks use keystream words 0..3");
 

@@ -40,6 +40,7 @@
 #include <stdint.h>
 
 #include "cz_device.h"
+#include "cz_diag.h"
 #include "../../include/curvezmq_mi355x.h"
 
 using namespace cz;
@@ -98,11 +99,7 @@ constexpr int BLOCK = 256;              // threads per workgroup (4 waves)
 #define CZ_SEG_OCC
 #endif
 constexpr int WAVES = BLOCK / 64;
-#ifdef CZ_FLUSH2
-constexpr u32 LINE_LDS_BYTES = 64 * 256; // EmitLines2 (A/B build): two 128-byte lines per frame
-#else
 constexpr u32 LINE_LDS_BYTES = 64 * 128; // EmitLines: one 128-byte line per frame
-#endif
 constexpr u32 HOLD_LDS_BYTES = 64 * 64;  // EmitLines (seal): block 1 of every frame, until tag()
 constexpr u32 REGION_MAX = 16384;       // EmitRegion: 64 slots per wave
 
@@ -115,16 +112,6 @@ __device__ __forceinline__ V4 zero4() { return V4{0u, 0u, 0u, 0u}; }
 // Byte-granular pieces of a 16-byte unit.  gfx950 executes unaligned global and LDS
 // accesses (the compiler emits them for align-1 types), so a clipped edge unit leaves in at
 // most 4 stores (8, 4, 2, 1 bytes) instead of a byte loop.
-// EmitShiftLines' chunk writes at byte offsets: 0 = dword funnel (alignbyte + 17 ds_write_b32),
-// 1 = ds_write_b128 at the byte address for outputs off 8-byte alignment, 2 = also for 8-byte ones
-#ifndef CZ_ULDS
-#define CZ_ULDS 1
-#endif
-// inputs at any byte offset: 1 = 16-byte global loads at the byte address (the hardware's
-// unaligned access) instead of dword-aligned loads and a byte funnel
-#ifndef CZ_UGLD
-#define CZ_UGLD 0
-#endif
 typedef uint64_t u64_ua __attribute__((aligned(1)));
 typedef uint32_t u32_ua __attribute__((aligned(1)));
 typedef uint16_t u16_ua __attribute__((aligned(1)));
@@ -172,9 +159,7 @@ __device__ __forceinline__ void buf_store16(u64 base, u32 voff, uint4 v)
 {
     const __amdgpu_buffer_rsrc_t rs =
         __builtin_amdgcn_make_buffer_rsrc(reinterpret_cast<void *>((uintptr_t)base), 0, (int)0xffffffffu, 0x00020000);
-#ifdef CZ_DIAG_NOSTORE_ALL  // timing diagnostic only: every emitter's line stores dropped (wrong output)
-    if (v.x == 0x13579bdfu && v.w == 0x2468ace0u)
-#endif
+    CZ_DIAG_STORE_GUARD(v)  // (cz_diag.h: compiled out of the product library)
     __builtin_amdgcn_raw_buffer_store_b128(v4u_t{v.x, v.y, v.z, v.w}, rs, (int)voff, 0, CP);
 }
 
@@ -257,23 +242,10 @@ __device__ __forceinline__ u32 ld32(const uint8_t *__restrict__ p)
         return (u32)p[0] | ((u32)p[1] << 8) | ((u32)p[2] << 16) | ((u32)p[3] << 24);
 }
 
-// Diagnostic builds only (tools/gpu_clock_ab.sh; never the shipped library, and their output
-// is wrong by construction): CZ_DIAG_NOLOAD makes full-chunk payload loads return address bits,
-// CZ_DIAG_NOSTORE drops EmitLines' line stores (kept for one impossible value), so the clock
-// and time of the 4k seal can be measured without its HBM reads or writes; CZ_DIAG_NOTAG writes
-// line 0 whole in the flush and drops the late 16-byte tag store; CZ_DIAG_L2STORE sends every
-// line store of a wave to the same 8 KiB (L2-resident, no HBM writes).
-
 // Unguarded full-chunk load (caller proved all 16 bytes valid).
 template <bool AL>
 __device__ __forceinline__ V4 ld16f(const uint8_t *__restrict__ p)
 {
-#ifdef CZ_DIAG_NOLOAD
-    if constexpr (AL) {
-        const u32 a = (u32)(uintptr_t)p;
-        return V4{a, a ^ 0x9e3779b9u, a + 0x7f4a7c15u, a ^ 0x85ebca6bu};
-    }
-#endif
     if constexpr (AL) {
         uint4 v = *reinterpret_cast<const uint4 *>(p);
         return V4{v.x, v.y, v.z, v.w};
@@ -285,31 +257,16 @@ __device__ __forceinline__ V4 ld16f(const uint8_t *__restrict__ p)
 // 8-byte aligned input (the open of bodies packed at 8-byte offsets): a
 // 16-byte chunk as two naturally aligned 8-byte loads.  ld16_8 reads the second half only when the
 // object reaches into it (an aligned 8-byte piece holding a valid byte cannot cross a page).
-// the seal's payload loads: non-temporal with CZ_SEAL_LOAD_NT (A/B), ld16f otherwise
-#ifndef CZ_SEAL_LOAD_NT
-#define CZ_SEAL_LOAD_NT 0
-#endif
+// the seal's payload loads (non-temporal loads measured -27..-35% on every seal: DESIGN.md section 6)
 template <bool AL>
 __device__ __forceinline__ V4 ld16f_in(const uint8_t *__restrict__ p)
 {
-#if CZ_SEAL_LOAD_NT
-    if constexpr (AL) {
-        const v4u_t v = __builtin_nontemporal_load(reinterpret_cast<const v4u_t *>(p));
-        return V4{v.x, v.y, v.z, v.w};
-    }
-#endif
     return ld16f<AL>(p);
 }
 __device__ __forceinline__ V4 ld16f_8(const uint8_t *__restrict__ p)
 {
-#ifdef CZ_AL8_X4
-    // one dword-aligned 16-byte load (as the uniform open's INA 8 path) instead of two
-    const uint4 r = *reinterpret_cast<const u4_a4 *>(p);
-    return V4{r.x, r.y, r.z, r.w};
-#else
     const uint2 a = reinterpret_cast<const uint2 *>(p)[0], b = reinterpret_cast<const uint2 *>(p)[1];
     return V4{a.x, a.y, b.x, b.y};
-#endif
 }
 __device__ __forceinline__ V4 ld16_8(const uint8_t *__restrict__ p, u64 avail)
 {
@@ -432,10 +389,6 @@ struct EmitLinesT {
     {
         const u32 c = lane & 7u;
         const u32 r = lane >> 3;
-#ifdef CZ_DIAG_L2STORE
-        uint8_t *p = wbase + 128u * r + 16u * c;  // every line of the wave onto its first 8 KiB
-        const u64 step = 1024u;  // (diagnostic build: plain stores)
-#else
         // A buffer store (buf_store16): the j-th frame group's line base lb + j * 8 * stride in
         // the resource (SGPRs, advanced by the scalar unit), this lane's 32-bit offset in a VGPR
         // computed once -- no VALU address arithmetic at all per store (plain C stores cost a
@@ -447,32 +400,16 @@ struct EmitLinesT {
         const u64 lb = uniform64((u64)(uintptr_t)wbase) + 128ull * line;
         const u32 voff = r * (u32)stride + 16u * c;
         const u32 step = 8u * (u32)stride;
-#endif
-#ifdef CZ_DIAG_NOTAG
-        const bool skip = false;
-#else
         // seal: line 0 leaves whole from close(), one full 128-byte line written once, not a
         // 112-byte line and a late 16-byte tag (partial lines cost L2 fills)
         const bool skip = tag_slot && line == 0 && !whole;
-#endif
         asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // the other lanes' ds_writes of this line
 #pragma unroll
         for (u32 j = 0; j < 8; j++) {
             const u32 F = 8u * j + r;
             uint4 v = lds[F * 8u + (c ^ (F & 7u))];
-#ifdef CZ_DIAG_NOSTORE
-            if (!skip && v.x == 0x13579bdfu && v.w == 0x2468ace0u)
-#else
             if (!skip)
-#endif
-#ifdef CZ_DIAG_L2STORE
-            {
-                *reinterpret_cast<uint4 *>(p) = v;
-            }
-            p += step;
-#else
                 buf_store16<CP>(lb + (u64)(j * step), voff, v);
-#endif
         }
     }
     __device__ __forceinline__ void emit(u32 q, const u32 Din[16])
@@ -513,14 +450,9 @@ struct EmitLinesT {
     }
     __device__ __forceinline__ void tag(const u32 t[4])
     {
-#ifdef CZ_DIAG_NOTAG
-        if (t[0] == 0x13579bdfu && t[3] == 0x2468ace0u)
-            *reinterpret_cast<uint4 *>(mine + 16) = make_uint4(t[0], t[1], t[2], t[3]);
-#else
 #pragma unroll
         for (int k = 0; k < 4; k++)
             tagw[k] = t[k];
-#endif
     }
     // seal, converged, after the last line's flush: line 0 = block 0 (header, nonce, tag,
     // 32 ciphertext bytes) + block 1 (held in LDS; zero if the frame has one block), staged
@@ -556,10 +488,8 @@ struct EmitLinesT {
     __device__ __forceinline__ void close(bool bad)
     {
         finish();
-#ifndef CZ_DIAG_NOTAG
         if (tag_slot)
             line0();
-#endif
         if (bad)
             poison();
     }
@@ -574,135 +504,6 @@ struct EmitLinesT {
 using EmitLines = EmitLinesT<CZ_OPEN_STORE_CPOL>;
 using EmitLinesSeal = EmitLinesT<CZ_SEAL_STORE_CPOL>;
 
-#ifdef CZ_FLUSH2
-// A/B build only (-DCZ_FLUSH2, DESIGN.md section 6, "the write-path clock"): EmitLines for the
-// seal with TWO lines per store instruction.  Rows are 256 bytes (16 units) per frame, a flush
-// every 4 chunks stores lines 2lp and 2lp+1 of the 64 frames as 16 global_store_dwordx4 of 4
-// frames x 256 bytes (EmitLines: 8 instructions of 8 frames x 128 bytes every 2 chunks).  Line 0
-// still leaves whole with the tag from close() (single-line store).  16 KiB of LDS per wave: 2 waves
-// per SIMD.
-struct EmitLines2 {
-    static constexpr bool cooperative = true;
-    uint4 *lds;        // this wave's 64 x 16 units
-    uint8_t *wbase;
-    uint8_t *mine;
-    u64 stride;
-    u32 lane, total, last_q;
-    bool tag_slot;
-    uint4 *hold;
-    u32 head[12];
-    u32 tagw[4];
-
-    // lines 2lp (first) and / or 2lp+1 (second) of the wave's 64 frames
-    __device__ __forceinline__ void flush_pair(u32 lp, bool first, bool second)
-    {
-        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // the other lanes' ds_writes of these lines
-        const u64 base = uniform64((u64)(uintptr_t)wbase) + 256ull * lp;
-        if (first && second) {
-            const u32 u = lane & 15u, r = lane >> 4;
-            const u32 voff = r * (u32)stride + 16u * u;
-            const u32 step = 4u * (u32)stride;
-#pragma unroll
-            for (u32 j = 0; j < 16; j++) {
-                const u32 F = 4u * j + r;
-                buf_store16(base + (u64)(j * step), voff, lds[F * 16u + (u ^ (F & 15u))]);
-            }
-        } else {
-            const u32 half = first ? 0u : 1u;
-            const u32 c = lane & 7u, r = lane >> 3;
-            const u32 voff = r * (u32)stride + 16u * c;
-            const u32 step = 8u * (u32)stride;
-#pragma unroll
-            for (u32 j = 0; j < 8; j++) {
-                const u32 F = 8u * j + r;
-                buf_store16(base + 128ull * half + (u64)(j * step), voff, lds[F * 16u + ((8u * half + c) ^ (F & 15u))]);
-            }
-        }
-    }
-    __device__ __forceinline__ void emit(u32 q, const u32 Din[16])
-    {
-        u32 D[16];
-#pragma unroll
-        for (int k = 0; k < 16; k++)
-            D[k] = Din[k];
-        if (64u * q + 64u > total)
-            mask_chunk(D, total > 64u * q ? total - 64u * q : 0u);
-        emit_full(q, D);
-    }
-    __device__ __forceinline__ void emit_full(u32 q, const u32 D[16])
-    {
-        if (tag_slot && q == 0u) {
-#pragma unroll
-            for (int k = 0; k < 4; k++)
-                head[k] = D[k];
-#pragma unroll
-            for (int k = 0; k < 8; k++)
-                head[4 + k] = D[8 + k];
-        }
-        if (tag_slot && q == 1u) {
-#pragma unroll
-            for (u32 c = 0; c < 4; c++)
-                hold[lane * 4u + c] = make_uint4(D[4 * c], D[4 * c + 1], D[4 * c + 2], D[4 * c + 3]);
-        }
-        const u32 pos = 4u * (q & 3u);
-        const u32 sw = lane & 15u;
-#pragma unroll
-        for (u32 c = 0; c < 4; c++)
-            lds[lane * 16u + ((pos + c) ^ sw)] = make_uint4(D[4 * c], D[4 * c + 1], D[4 * c + 2], D[4 * c + 3]);
-        if ((q & 3u) == 3u)
-            flush_pair(q >> 2, !(tag_slot && q == 3u), true);
-        last_q = q;
-    }
-    __device__ __forceinline__ void tag(const u32 t[4])
-    {
-#pragma unroll
-        for (int k = 0; k < 4; k++)
-            tagw[k] = t[k];
-    }
-    __device__ __forceinline__ void line0()
-    {
-        const u32 sw = lane & 15u;
-        const bool one = last_q == 0u;
-        uint4 b1[4];
-#pragma unroll
-        for (u32 c = 0; c < 4; c++)
-            b1[c] = one ? make_uint4(0u, 0u, 0u, 0u) : hold[lane * 4u + c];
-        lds[lane * 16u + (0u ^ sw)] = make_uint4(head[0], head[1], head[2], head[3]);
-        lds[lane * 16u + (1u ^ sw)] = make_uint4(tagw[0], tagw[1], tagw[2], tagw[3]);
-        lds[lane * 16u + (2u ^ sw)] = make_uint4(head[4], head[5], head[6], head[7]);
-        lds[lane * 16u + (3u ^ sw)] = make_uint4(head[8], head[9], head[10], head[11]);
-#pragma unroll
-        for (u32 c = 0; c < 4; c++)
-            lds[lane * 16u + ((4u + c) ^ sw)] = b1[c];
-        flush_pair(0, true, false);
-    }
-    // the last pair when it did not end on a 4-chunk boundary: zero the rest of the row and store
-    // the lines that hold chunks (the line of the last chunk is the slot's last written line, as
-    // in EmitLines)
-    __device__ __forceinline__ void finish()
-    {
-        const u32 r = last_q & 3u;
-        if (r == 3u)
-            return;
-        const u32 sw = lane & 15u;
-        const u32 done = 4u * (r + 1u), end = r < 2u ? 8u : 16u;
-        for (u32 u = done; u < end; u++)
-            lds[lane * 16u + (u ^ sw)] = make_uint4(0u, 0u, 0u, 0u);
-        const u32 lp = last_q >> 2;
-        const bool first = !(tag_slot && lp == 0u);
-        const bool second = r >= 2u;
-        if (first || second)
-            flush_pair(lp, first, second);
-    }
-    __device__ __forceinline__ void close(bool bad)
-    {
-        (void)bad;  // seal only
-        finish();
-        if (tag_slot)
-            line0();
-    }
-};
-#endif
 
 // Whole-region staging for a full wave of small equal-length frames: the wave's
 // 64 slots (64 * stride <= REGION_MAX, stride % 16 == 0) are assembled in LDS
@@ -924,9 +725,6 @@ __device__ __forceinline__ void seal_frame(const uint8_t *__restrict__ in0, u32 
                 // behind it, so a line is read in pieces and L2 re-fetches it: FETCH 1.20x the box
                 // bytes.  A sched_barrier here keeps the 8 loads together and the first wait ~1570
                 // instructions later -- and measured 14% SLOWER (interleaved A/B).)
-#ifdef CZ_BOX_FENCE
-                __builtin_amdgcn_sched_barrier(0);
-#endif
                 box_full_block(2u * k, L);
                 box_full_block(2u * k + 1u, L + 16);
                 blk = 2u * k + 2u;
@@ -1221,9 +1019,6 @@ __device__ __forceinline__ u32 open_frame(const uint8_t *__restrict__ in, u32 si
     auto LF = [&](u32 off) -> V4 {
         if constexpr (INA == 16) {
             return ld16f<AL>(in + off);
-        } else if constexpr (INA == 1 && CZ_UGLD) {
-            const v4u_t r = *reinterpret_cast<const v4u_ua *>(in + off);  // global_load_dwordx4 at the byte address
-            return V4{r.x, r.y, r.z, r.w};
         } else {
             const uint4 r = *reinterpret_cast<const u4_a4 *>(in4 + off);
             if constexpr (INA == 8)
@@ -1480,7 +1275,7 @@ __device__ __forceinline__ u32 open_frame(const uint8_t *__restrict__ in, u32 si
             }
             for (u32 k = 1; !CARRY && 2u * k + 1u < nfull; k++) {
                 u32 M[32];
-                if constexpr (INA == 1 && !CZ_UGLD) {
+                if constexpr (INA == 1) {
                     // 8 loads from the dword-aligned line below and the dword after it, funnelled
                     // inside open_block (after the keystream)
                     const uint8_t *src4 = in4 + 128u * k;
@@ -1721,7 +1516,6 @@ struct EmitShiftLinesT {
     u32 lane, total, last_q;
     u32 te;          // end of the output in its line space, d + total | bit 31: leave output bytes 16..31 to tag()
     u32 mixed;       // the wave holds outputs of both classes
-    u32 carry_w;     // the previous chunk's last dword (the first shifted dword of a chunk straddles both)
     u32 walign;      // largest of 16 / 8 / 1 that divides every output's line offset in the wave
     u64 ubase;       // UNI: the workgroup's first output address rounded down to 128 (wave-uniform)
     u32 loff[8];     // UNI: line offset from ubase of output F = 8j + lane / 8, plus 16 * (lane & 7)
@@ -1747,7 +1541,6 @@ struct EmitShiftLinesT {
     // the launchers keep d + total below 2^31
     __device__ __forceinline__ void init(bool tag_slot)
     {
-        carry_w = 0u;
         const u32 d = (u32)(uintptr_t)mine & 127u;
         walign = __builtin_amdgcn_ballot_w64((d & 15u) != 0u) == 0  ? 16u
                  : __builtin_amdgcn_ballot_w64((d & 7u) != 0u) == 0 ? 8u
@@ -1856,9 +1649,6 @@ struct EmitShiftLinesT {
     // for the next line (LDS ops of one wave execute in order: the flush's reads come first)
     __device__ __forceinline__ void shift_row(u32 end)
     {
-#ifdef CZ_DIAG_NOSHIFTROW  // timing diagnostic only: wrong output
-        return;
-#endif
         asm volatile("" ::: "memory");
         uint4 *row = reinterpret_cast<uint4 *>(rows + lane * SROW + SHEAD);
 #pragma unroll
@@ -1871,32 +1661,13 @@ struct EmitShiftLinesT {
     {
         const u32 t = ((u32)(uintptr_t)mine & 127u) + 64u * q;
         const u32 pos = t & 127u;
-        // chunk byte i belongs at line-space byte pos + i.  With b = (4 - (pos & 3)) & 3, dword k of
-        // E = alignbyte(D[k], D[k-1], b) (D[-1] = the previous chunk's last dword) holds line-space
-        // bytes [pos - 4 + b + 4k, +4): every write is dword-aligned.  E[16] is this chunk's tail;
-        // the next chunk's E[0] rewrites that dword whole.
-        // A wave whose offsets are all 16- or 8-byte multiples writes the chunk as it is, with
-        // ds_write_b128 / b64 at aligned addresses (no funnel); only the other waves pay it.
-#if CZ_ULDS
+        // chunk byte i belongs at line-space byte pos + i.  A wave whose offsets are all 16- or
+        // 8-byte multiples writes the chunk with ds_write_b128 / b64 at aligned addresses; the
+        // others with ds_write_b128 at the byte address (the dword funnel it replaced: DESIGN.md
+        // section 4, "Byte-address LDS writes").
         // ds_write_b128 at any byte address (ROCm runs LDS in unaligned mode; the hardware splits
         // the access): the chunk's bytes land exactly at [pos, pos + 64), no funnel, no tail dword
         const u32 b = 0u;
-        uint8_t *row0 = rows + lane * SROW + SHEAD;
-        if (walign == 16u) {
-#pragma unroll
-            for (u32 c = 0; c < 4; c++)
-                reinterpret_cast<uint4 *>(row0 + pos)[c] = make_uint4(D[4 * c], D[4 * c + 1], D[4 * c + 2], D[4 * c + 3]);
-        } else if (CZ_ULDS == 1 && walign == 8u) {
-#pragma unroll
-            for (u32 c = 0; c < 8; c++)
-                reinterpret_cast<uint2 *>(row0 + pos)[c] = make_uint2(D[2 * c], D[2 * c + 1]);
-        } else {
-#pragma unroll
-            for (u32 c = 0; c < 4; c++)
-                *reinterpret_cast<v4u_ua *>(row0 + pos + 16u * c) = v4u_t{D[4 * c], D[4 * c + 1], D[4 * c + 2], D[4 * c + 3]};
-        }
-#else
-        const u32 b = (4u - (pos & 3u)) & 3u;
         uint8_t *row0 = rows + lane * SROW + SHEAD;
         if (walign == 16u) {
 #pragma unroll
@@ -1907,15 +1678,10 @@ struct EmitShiftLinesT {
             for (u32 c = 0; c < 8; c++)
                 reinterpret_cast<uint2 *>(row0 + pos)[c] = make_uint2(D[2 * c], D[2 * c + 1]);
         } else {
-            u32 *w = reinterpret_cast<u32 *>(row0 + pos + b - 4u);
-            w[0] = funnel(D[0], carry_w, b);
 #pragma unroll
-            for (u32 k = 1; k < 16; k++)
-                w[k] = funnel(D[k], D[k - 1], b);
-            w[16] = funnel(0u, D[15], b);
-            carry_w = D[15];
+            for (u32 c = 0; c < 4; c++)
+                *reinterpret_cast<v4u_ua *>(row0 + pos + 16u * c) = v4u_t{D[4 * c], D[4 * c + 1], D[4 * c + 2], D[4 * c + 3]};
         }
-#endif
         const bool done = (t & 64u) != 0u;
         if (mixed) {
             flush<FL_MIXED>(q);
@@ -2378,10 +2144,7 @@ __device__ __forceinline__ u32 open_segment(const uint8_t *__restrict__ in, u32 
     const u32 ina = ANY ? (u32)(uintptr_t)in & 3u : 0u;
     const uint8_t *in4 = in - ina;
     auto ldf = [&](const uint8_t *p) -> V4 {  // all 16 bytes inside the body
-        if constexpr (ANY && CZ_UGLD) {
-            const v4u_t r = *reinterpret_cast<const v4u_ua *>(p);
-            return V4{r.x, r.y, r.z, r.w};
-        } else if constexpr (ANY) {
+        if constexpr (ANY) {
             const uint8_t *q = in4 + (p - in);
             const uint4 r = *reinterpret_cast<const u4_a4 *>(q);
             const u32 r4 = ina ? *reinterpret_cast<const u32 *>(q + 16) : 0u;
@@ -2577,11 +2340,7 @@ __device__ __forceinline__ void seal_uniform_body(const uint8_t *__restrict__ in
         const u32 fl = (MODE == MODE_ZMQ && flags8) ? flags8[i] : 0u;
         const u32 lane = threadIdx.x & 63u;
         if constexpr (ST == ST_LINES) {
-#ifdef CZ_FLUSH2
-            using EmL = EmitLines2;
-#else
             using EmL = EmitLinesSeal;
-#endif
             EmL em{smem + (threadIdx.x >> 6) * (LINE_LDS_BYTES / 16), out + (uint64_t)wave_first * out_stride,
                    dst, out_stride, lane, mlen, 0u, true,
                    smem + (WAVES * LINE_LDS_BYTES + (threadIdx.x >> 6) * HOLD_LDS_BYTES) / 16};
@@ -3847,11 +3606,7 @@ hipError_t czk_seal_segments(const cz_frame_desc *desc, const cz_segment *segs, 
                              uint32_t ncomb, const void *in, void *out, const void *subkeys, void *work, hipStream_t s)
 {
     const dim3 grid((nseg + BLOCK - 1) / BLOCK);
-#ifdef CZ_SEG_SINGLE_KERNEL  // A/B: one k_seal_segments launch for every wave
-    if (false) {
-#else
     if (nseg && g_seglines && g_pair) {
-#endif
         const int mode = SEGMODE_LINES | SEGMODE_PAIR | (g_shift16 ? SEGMODE_SHIFT16 : 0) | (g_seal_ina ? SEGMODE_ANYIN : 0);
         hipLaunchKernelGGL(k_seal_segments_lines, grid, dim3(BLOCK), WAVES * SHIFT_LDS_BYTES, s, desc, segs, nseg,
                            (const uint8_t *)in, (uint8_t *)out, (const uint8_t *)subkeys, (u32 *)work, mode);

@@ -114,9 +114,32 @@ def launch_ranks(gpus, argv, popen=None):
         print(f"rank line does not cover {gpus} GPUs: n_gpus={line.get('n_gpus')}, per_rank={len(per)}",
               file=sys.stderr)
         return 1
+    # an N > 1 line is as self-describing as the N = 1 line: the roofline from the slowest rank's
+    # kernel time (with the per-rank spread) and the CPU baseline
+    roof = line.get("roofline") or {}
+    missing = [k for k in ("achieved", "frac", "frac_min", "frac_max", "kernel_ms_max") if roof.get(k) is None]
+    if "--no-cpu-baseline" not in argv and not line.get("cpu_baseline"):
+        missing.append("cpu_baseline")
+    if line.get("value") is not None and missing:
+        print(f"rank line lacks {missing}", file=sys.stderr)
+        return 1
     line["launcher"] = "bench.py --gpus: child torch.distributed.run"
     print(json.dumps(line), flush=True)
     return 0
+
+
+def multi_rank_roofline(kernel_s, alg_bytes):
+    """The N > 1 line's roofline: `achieved` / `frac` / `kernel_ms` from the SLOWEST rank's average
+    kernel time (the one that sets the job's time), with the fastest and slowest ranks' fractions
+    beside it.  kernel_s: every rank's average kernel time in seconds."""
+    slow, fast = max(kernel_s), min(kernel_s)
+    achieved = alg_bytes / slow / 1e9
+    return {"achieved": round(achieved, 2), "frac": round(achieved / HBM_PEAK_GBS, 4),
+            "kernel_ms": round(slow * 1e3, 4), "kernel_ms_min": round(fast * 1e3, 4),
+            "kernel_ms_max": round(slow * 1e3, 4),
+            "frac_min": round(alg_bytes / slow / 1e9 / HBM_PEAK_GBS, 4),
+            "frac_max": round(alg_bytes / fast / 1e9 / HBM_PEAK_GBS, 4),
+            "kernel_time_from": "slowest rank (per-rank figures in per_rank)"}
 
 
 def setup_dist(args):
@@ -961,7 +984,7 @@ def main():
     kern_ms = [a.elapsed_time(b) for a, b in evs]
     avg_kernel_s = float(np.mean(kern_ms)) / 1e3
 
-    per_rank = None
+    per_rank, kernel_s = None, [avg_kernel_s]
     if world > 1:
         # every rank's own kernel time and roofline fraction (the driver's 1/2/4/8-GPU runs then
         # carry absolute per-GPU figures with no further code change)
@@ -971,14 +994,17 @@ def main():
         allk = [torch.zeros(1, dtype=torch.float64, device=kd) for _ in range(world)]
         dist.all_gather(allk, mine)
         alg = wl.read_bytes + wl.write_bytes
-        per_rank = [{"rank": r, "kernel_ms": round(float(k.item()) * 1e3, 4),
-                     "payload_GiBps": round(wl.payload_bytes / float(k.item()) / 2**30, 2),
-                     "hbm_frac": round(alg / float(k.item()) / 1e9 / HBM_PEAK_GBS, 4)} for r, k in enumerate(allk)]
+        kernel_s = [float(k.item()) for k in allk]
+        per_rank = [{"rank": r, "kernel_ms": round(k * 1e3, 4),
+                     "payload_GiBps": round(wl.payload_bytes / k / 2**30, 2),
+                     "hbm_frac": round(alg / k / 1e9 / HBM_PEAK_GBS, 4)} for r, k in enumerate(kernel_s)]
     elapsed = max_over_ranks(world, elapsed)
     total_payload = sum_over_ranks(world, float(wl.payload_bytes) * args.steps)
     value = total_payload / elapsed / 2**30
     alg_bytes = wl.read_bytes + wl.write_bytes
-    achieved = alg_bytes / avg_kernel_s / 1e9
+    roof_k = multi_rank_roofline(kernel_s, alg_bytes)  # N = 1: this rank's own kernel time
+    achieved = roof_k["achieved"]
+    slow_kernel_s = max(kernel_s)
     copy_gbs, torch_copy_gbs = hbm_copy_ceiling(dev) if rank == 0 else (None, None)
     sys.path.insert(0, os.path.join(ROOT, "tools"))
     from pmc_key import key_from_args
@@ -995,8 +1021,12 @@ def main():
         rtl = roundtrip_leg(wl, world, min(args.steps, 10))
 
     cpu = None
-    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+    if rank == 0 and not args.no_cpu_baseline:
+        # at N > 1 too, on rank 0 after every timed leg (the other ranks wait at the barrier below)
         cpu = cpu_baseline(wl, args.cpu_seconds)
+        if world > 1:
+            cpu["measured"] = f"rank 0 of {world}, after the timed region"
+    barrier(world)
 
     if rank == 0:
         names = {"4k": "1M x 4 KiB frames, seal (configs[1])",
@@ -1034,10 +1064,10 @@ def main():
                        "frames_per_s": round(wl.count * world * args.steps / elapsed, 1)},
             # bound: the roof that binds is VALU issue; achieved / peak / frac are the
             # HBM figures the north star asks for, the VALU roof is in "valu"
-            "roofline": {"bound": "valu", "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                         "frac": round(achieved / HBM_PEAK_GBS, 4),
+            "roofline": {"bound": "valu", "achieved": roof_k["achieved"], "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                         "frac": roof_k["frac"],
                          "traffic": traffic,
-                         "kernel_ms": round(avg_kernel_s * 1e3, 4),
+                         **{k: v for k, v in roof_k.items() if k not in ("achieved", "frac")},
                          # the same bytes against the device-to-device copy rate
                          # measured on this GPU in this process (read + write bytes / time)
                          "hbm_copy_GBps": copy_gbs,  # cz_dev_copy (float4 copy kernel) of 2 GiB, 10 reps
@@ -1045,7 +1075,7 @@ def main():
                          "torch_copy_GBps": torch_copy_gbs,
                          "pmc_key": pmc_key,
                          "alg_bytes_per_launch": alg_bytes,
-                         "valu": valu_roofline(pmc, avg_kernel_s)},
+                         "valu": valu_roofline(pmc, slow_kernel_s)},
             "cpu_baseline": cpu,
         }
         if rtl is not None:

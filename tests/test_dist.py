@@ -193,10 +193,15 @@ class _FakePopen:
         return self.rc
 
 
-def _rank_line(n):
+def _rank_line(n, roofline=True, cpu=True):
     import json
-    return json.dumps({"metric": "m", "value": 1.0, "n_gpus": n,
-                       "per_rank": [{"rank": r, "kernel_ms": 2.0} for r in range(n)]}) + "\n"
+    import bench
+    line = {"metric": "m", "value": 1.0, "n_gpus": n, "per_rank": [{"rank": r, "kernel_ms": 2.0} for r in range(n)]}
+    if roofline:
+        line["roofline"] = bench.multi_rank_roofline([2e-3 + 1e-5 * r for r in range(n)], 8.6e9)
+    if cpu:
+        line["cpu_baseline"] = {"value": 0.5, "unit": "GiB/s", "cores": 1, "kind": "port", "sample": "s"}
+    return json.dumps(line) + "\n"
 
 
 def test_bench_gpus_n_launches_child_ranks_without_touching_gpu(capsys):
@@ -223,12 +228,26 @@ def test_bench_gpus_n_launches_child_ranks_without_touching_gpu(capsys):
     ([_rank_line(2), _rank_line(2)], 0),     # more than one JSON line
     ([], 0),                                 # no line at all
     ([_rank_line(2)], 3),                    # a rank failed: its exit status is passed on
+    ([_rank_line(2, roofline=False)], 0),    # N > 1 line without the slowest-rank roofline
+    ([_rank_line(2, cpu=False)], 0),         # N > 1 line without the CPU baseline
 ])
 def test_bench_launcher_rejects_bad_rank_output(out, rc, capsys):
     import bench
     got = bench.launch_ranks(2, ["--gpus", "2"], popen=_FakePopen(out, rc))
     assert got == (rc if rc else 1)
     assert not [ln for ln in capsys.readouterr().out.splitlines() if ln.startswith("{")]
+
+
+def test_multi_rank_roofline_uses_the_slowest_rank():
+    """at N > 1, achieved / frac come from the slowest rank's kernel time (it sets
+    the job's time), with the per-rank min and max fractions beside it."""
+    import bench
+    r = bench.multi_rank_roofline([2.0e-3, 2.5e-3, 2.1e-3], 8e9)
+    assert r["kernel_ms"] == r["kernel_ms_max"] == 2.5 and r["kernel_ms_min"] == 2.0
+    assert r["achieved"] == 3200.0 and r["frac"] == round(3200.0 / bench.HBM_PEAK_GBS, 4) == r["frac_min"]
+    assert r["frac_max"] == round(4000.0 / bench.HBM_PEAK_GBS, 4)
+    one = bench.multi_rank_roofline([2.0e-3], 8e9)
+    assert one["frac"] == one["frac_min"] == one["frac_max"]
 
 
 def test_bench_refuses_world_size_mismatch(monkeypatch):

@@ -101,13 +101,18 @@ def test_bench_ws2_rehearsal():
     env = dict(os.environ, CZ_DIST_BACKEND="gloo", TMPDIR="/tmp")
     cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2", "--master-addr",
            "127.0.0.1", "--master-port", str(_free_port()), os.path.join(ROOT, "bench.py"), "--gpus", "2",
-           "--steps", "3", "--warmup", "1", "--ramp-ms", "0", "--frames", "65536"]
+           "--steps", "3", "--warmup", "1", "--ramp-ms", "0", "--frames", "65536", "--cpu-seconds", "1"]
     r = subprocess.run(cmd, capture_output=True, text=True, timeout=300, env=env, cwd=ROOT)
     assert r.returncode == 0, r.stderr[-3000:]
     lines = [ln for ln in r.stdout.splitlines() if ln.startswith("{")]
     assert len(lines) == 1, r.stdout[-2000:]
     line = json.loads(lines[0])
     assert line["n_gpus"] == 2 and line["scaling"] == "weak"
+    # as self-describing as the N = 1 line: slowest-rank roofline with its spread, and the CPU baseline
+    roof = line["roofline"]
+    assert roof["kernel_ms"] == roof["kernel_ms_max"] == max(p["kernel_ms"] for p in line["per_rank"])
+    assert roof["frac_min"] <= roof["frac"] <= roof["frac_max"] and roof["frac"] == roof["frac_min"]
+    assert line["cpu_baseline"]["value"] > 0 and "rank 0 of 2" in line["cpu_baseline"]["measured"]
     assert line["scatter_gather"]["verified"] and line["seal_open_verify"]["verified"]
     assert [p["rank"] for p in line["per_rank"]] == [0, 1]
     assert all(p["hbm_frac"] > 0 for p in line["per_rank"])
@@ -124,7 +129,7 @@ def test_bench_plain_gpus2_launches_its_own_ranks():
     for k in ("WORLD_SIZE", "RANK", "LOCAL_RANK", "MASTER_ADDR", "MASTER_PORT"):
         env.pop(k, None)
     cmd = [sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "2", "--steps", "3", "--warmup", "1",
-           "--ramp-ms", "0", "--frames", "65536"]
+           "--ramp-ms", "0", "--frames", "65536", "--cpu-seconds", "1"]
     r = subprocess.run(cmd, capture_output=True, text=True, timeout=300, env=env, cwd=ROOT)
     assert r.returncode == 0, r.stderr[-3000:]
     lines = [ln for ln in r.stdout.splitlines() if ln.startswith("{")]

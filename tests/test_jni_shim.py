@@ -123,6 +123,97 @@ def test_shim_compiles_and_exports_every_native(shim):
     assert declared == set(NATIVES), declared ^ set(NATIVES)
 
 
+def _java_sources():
+    import re
+    out = {}
+    for dp, _, files in os.walk(os.path.join(JNI, "java")):
+        for f in files:
+            if f.endswith(".java"):
+                out[os.path.relpath(os.path.join(dp, f), os.path.join(JNI, "java"))] = open(os.path.join(dp, f)).read()
+    return out
+
+
+def test_java_callers_call_only_declared_natives():
+    """The Java callers (PinnedMsgAllocator, GpuCurveIoHook, GpuCurveMessageBatch, the GPU CURVE
+    mechanisms) cannot be compiled here (no JDK): check that every GpuCurveEngine / GpuCurveBatch call
+    they make names a native the classes declare -- and so, by the mangling test above, a symbol the
+    shim exports -- with the declared number of arguments; that each file's package and class match
+    its path; and that braces and parentheses balance outside comments and strings."""
+    import re
+    srcs = _java_sources()
+    natives = {}
+    for path, src in srcs.items():
+        cls = os.path.basename(path)[:-len(".java")]
+        for ret, meth, args in re.findall(r"static native ([\w\[\]]+) (\w+)\(([^)]*)\)", src):
+            natives[(cls, meth)] = len([a for a in args.split(",") if a.strip()])
+    calls = 0
+    for path, src in srcs.items():
+        code = re.sub(r"//[^\n]*|\"(?:\\.|[^\"\\])*\"", "", src)
+        pkg = re.search(r"^package ([\w.]+);", src, re.M).group(1)
+        assert path == os.path.join(*pkg.split("."), os.path.basename(path)), path
+        cls = os.path.basename(path)[:-len(".java")]
+        assert re.search(r"\b(class|interface) " + cls + r"\b", code), path
+        assert code.count("{") == code.count("}") and code.count("(") == code.count(")"), path
+        for m in re.finditer(r"\b(GpuCurveEngine|GpuCurveBatch)\.(\w+)\(", code):
+            owner, meth = m.group(1), m.group(2)
+            assert (owner, meth) in natives, (path, owner, meth)
+            # count the call's top-level arguments
+            depth, i, nargs, start = 1, m.end(), 0, m.end()
+            while depth:
+                ch = code[i]
+                depth += ch in "([{"
+                depth -= ch in ")]}"
+                if ch == "," and depth == 1:
+                    nargs += 1
+                i += 1
+            nargs += 1 if code[start:i - 1].strip() else 0
+            assert nargs == natives[(owner, meth)], (path, owner, meth, nargs)
+            calls += 1
+    assert calls >= 20
+    for f in ("zmq/io/GpuCurveIoHook.java", "zmq/io/mechanism/curve/PinnedMsgAllocator.java",
+              "zmq/io/mechanism/curve/GpuCurveMessageBatch.java", "zmq/io/mechanism/curve/GpuCurveClientMechanism.java",
+              "zmq/io/mechanism/curve/GpuCurveServerMechanism.java"):
+        assert f in srcs, f
+
+
+REF_JAVA = "/root/reference/jeromq-core/src/main/java/zmq"
+
+
+@pytest.mark.skipif(not os.path.isdir(REF_JAVA), reason="reference sources not present (build container only)")
+def test_java_callers_use_reference_api_that_exists():
+    """Every JeroMQ member the Java callers rely on exists in the reference with that signature
+    (read as text: the reference is never built or run here)."""
+    need = {
+        "Msg.java": ["public Msg(final ByteBuffer src)", "public Msg(byte[] src)", "public Msg(int capacity)",
+                     "public boolean hasMore()", "public boolean isCommand()", "public void setFlags(int flags)",
+                     "public ByteBuffer buf()", "public int size()", "public Msg put(ByteBuffer src, int off, int len)",
+                     "public static final int MORE", "public static final int COMMAND"],
+        "msg/MsgAllocator.java": ["Msg allocate(int size);"],
+        "msg/MsgAllocatorHeap.java": ["public class MsgAllocatorHeap implements MsgAllocator"],
+        "io/SessionBase.java": ["public SocketBase getSocket()", "public String getEndpoint()"],
+        "SocketBase.java": ["public final void eventHandshakeFailedProtocol(String addr, int errno)"],
+        "Options.java": ["public final Errno errno", "public boolean asServer"],
+        "util/Errno.java": ["public void set(int errno)"],
+        "io/mechanism/Mechanism.java": ["protected final SessionBase session;", "public Msg decode(Msg msg)",
+                                        "public Msg encode(Msg msg)", "public abstract Status status();"],
+        "io/mechanism/curve/CurveClientMechanism.java": ["public class CurveClientMechanism extends Mechanism",
+                                                         "public CurveClientMechanism(SessionBase session, Options options)",
+                                                         "private final byte[] cnPrecom", "private long cnNonce;",
+                                                         "private long cnPeerNonce;"],
+        "io/mechanism/curve/CurveServerMechanism.java": [
+            "public class CurveServerMechanism extends Mechanism",
+            "public CurveServerMechanism(SessionBase session, Address peerAddress, Options options)",
+            "private final byte[] cnPrecom", "private long cnNonce;", "private long cnPeerNonce;"],
+        "ZMQ.java": ["ZMQ_PROTOCOL_ERROR_ZMTP_UNEXPECTED_COMMAND ", "ZMQ_PROTOCOL_ERROR_ZMTP_MALFORMED_COMMAND_MESSAGE ",
+                     "ZMQ_PROTOCOL_ERROR_ZMTP_CRYPTOGRAPHIC ", "ZMQ_PROTOCOL_ERROR_ZMTP_INVALID_SEQUENCE "],
+        "ZError.java": ["public static final int EPROTO"],
+    }
+    for f, members in need.items():
+        text = open(os.path.join(REF_JAVA, f)).read()
+        for m in members:
+            assert m in text, (f, m)
+
+
 @pytest.mark.parametrize("case", ["short_c", "short_m", "short_nonce", "short_key", "mlen_below_32", "null_m"])
 def test_jnacl_length_guards_pin_nothing(shim, case):
     L = shim

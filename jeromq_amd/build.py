@@ -23,7 +23,8 @@ ROOT = os.path.dirname(HERE)
 CSRC = os.path.join(HERE, "csrc")
 PRODUCT_LIB = os.path.join(HERE, "libcurvezmq_mi355x.so")
 LIB = os.environ.get("CZ_LIB_OUT", PRODUCT_LIB)
-SOURCES = ["cz_kernels.hip", "cz_x25519.hip", "cz_host.cpp", "cz_mechanism.cpp", "cz_wire.cpp", "cz_engine.cpp", "cz_handshake.cpp", "cz_curve_hs.cpp"]
+# "file#n": the file compiled with -DCZ_KPART=n (cz_kernels.hip builds as three parts in parallel)
+SOURCES = ["cz_kernels.hip#1", "cz_kernels.hip#2", "cz_kernels.hip#3", "cz_x25519.hip", "cz_host.cpp", "cz_mechanism.cpp", "cz_wire.cpp", "cz_engine.cpp", "cz_handshake.cpp", "cz_curve_hs.cpp"]
 HEADERS = ["cz_device.h", "cz_diag.h", "cz_internal.h", "cz_salsa_lazy.h", "cz_salsa_tail.h", os.path.join("..", "..", "include", "curvezmq_mi355x.h")]
 ARCH = os.environ.get("CZ_OFFLOAD_ARCH", "gfx950")
 LLVM_BIN = "/opt/rocm/lib/llvm/bin"
@@ -58,7 +59,7 @@ def _stale(lib=LIB, sources=SOURCES):
     if not os.path.exists(lib):
         return True
     t = os.path.getmtime(lib)
-    return any(os.path.getmtime(os.path.join(CSRC, f)) > t for f in list(sources) + HEADERS)
+    return any(os.path.getmtime(os.path.join(CSRC, f.split("#")[0])) > t for f in list(sources) + HEADERS)
 
 
 def device_code_objects(so_path, arch=ARCH):
@@ -135,9 +136,10 @@ def build_library(force=False, verbose=True, sources=None, lib=None, src_dir=Non
     common = compile_flags(lib)
     objdir = tempfile.mkdtemp(prefix="cz_build_")
     try:
-        def compile_one(f):
-            obj = os.path.join(objdir, os.path.splitext(f)[0] + ".o")
-            cmd = [hipcc] + common + ["-c", "-o", obj, os.path.join(src_dir, f)]
+        def compile_one(entry):
+            f, _, part = entry.partition("#")
+            obj = os.path.join(objdir, os.path.splitext(f)[0] + (f"_{part}" if part else "") + ".o")
+            cmd = [hipcc] + common + ([f"-DCZ_KPART={part}"] if part else []) + ["-c", "-o", obj, os.path.join(src_dir, f)]
             if verbose:
                 print(" ".join(cmd), file=sys.stderr)
             r = subprocess.run(cmd, cwd=src_dir, capture_output=True, text=True)
@@ -147,7 +149,7 @@ def build_library(force=False, verbose=True, sources=None, lib=None, src_dir=Non
                 raise subprocess.CalledProcessError(r.returncode, cmd, r.stdout, r.stderr)
             return obj
         # the largest translation unit first: the kernels dominate the build
-        order = sorted(sources, key=lambda f: -os.path.getsize(os.path.join(src_dir, f)))
+        order = sorted(sources, key=lambda f: -os.path.getsize(os.path.join(src_dir, f.split("#")[0])))
         with ThreadPoolExecutor(max_workers=jobs or min(len(order), os.cpu_count() or 4, 8)) as ex:
             objs = list(ex.map(compile_one, order))
         tmp = f"{lib}.{os.getpid()}.tmp"  # (concurrent builds, e.g. pytest -n, never share a file)

@@ -39,9 +39,19 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+#include <type_traits>
+
 #include "cz_device.h"
 #include "cz_diag.h"
 #include "../../include/curvezmq_mi355x.h"
+
+// The file compiles as one translation unit (CZ_KPART undefined) or as three that build in parallel
+// (jeromq_amd/build.py: -DCZ_KPART=1 the uniform seal kernels and launchers, 2 the uniform opens,
+// 3 everything else and the run-time knobs); each part instantiates only its own kernels.
+#ifndef CZ_KPART
+#define CZ_KPART 0
+#endif
+#define CZ_KPART_HAS(n) (CZ_KPART == 0 || CZ_KPART == (n))
 
 using namespace cz;
 
@@ -656,8 +666,9 @@ __device__ __forceinline__ void seal_frame(const uint8_t *__restrict__ in0, u32 
     Poly P;
     poly_init(P, x[0], x[1], x[2], x[3], x[4], x[5], x[6], x[7]);
 
-    // ZMQ, one full block b >= 1 from its 17-dword window W = P[16b-9 .. 16b+7]
-    auto zmq_full_block = [&](u32 blk, const u32 *W) {
+    // ZMQ, one full block b >= 1 from its 17-dword window W = P[16b-9 .. 16b+7]; STEADY: a block of
+    // the pair loop (b >= 2), emitted through the emitter's steady-state form if it has one
+    auto zmq_block = [&](u32 blk, const u32 *W, auto steady) {
         ksblock(x, blk, 0u);
 #pragma unroll
         for (int k = 0; k < 16; k++)
@@ -666,8 +677,12 @@ __device__ __forceinline__ void seal_frame(const uint8_t *__restrict__ in0, u32 
         poly_block(P, C[4], C[5], C[6], C[7], 1u);
         poly_block(P, C[8], C[9], C[10], C[11], 1u);
         poly_block(P, C[12], C[13], C[14], C[15], 1u);
-        em.emit_full(blk, C);
+        if constexpr (decltype(steady)::value)
+            emit_steady(em, blk, C);
+        else
+            em.emit_full(blk, C);
     };
+    auto zmq_full_block = [&](u32 blk, const u32 *W) { zmq_block(blk, W, std::false_type{}); };
 
     // box-aligned input, one full block b >= 1 from its 16 dwords
     [[maybe_unused]] auto box_full_block = [&](u32 blk, const u32 *W) {
@@ -806,8 +821,8 @@ __device__ __forceinline__ void seal_frame(const uint8_t *__restrict__ in0, u32 
 #pragma unroll
                 for (int q = 0; q < 8; q++)
                     W[9 + q] = L[q];
-                zmq_full_block(2u * k, W);
-                zmq_full_block(2u * k + 1u, L + 7);
+                zmq_block(2u * k, W, std::true_type{});
+                zmq_block(2u * k + 1u, L + 7, std::true_type{});
 #pragma unroll
                 for (int q = 0; q < 9; q++)
                     cy[q] = L[23 + q];
@@ -1725,6 +1740,80 @@ using EmitShiftLinesUni = EmitShiftLinesT<true>;
 using EmitShiftLinesSeal = EmitShiftLinesT<false, CZ_SEAL_STORE_CPOL>;
 using EmitShiftLinesUniSeal = EmitShiftLinesT<true, CZ_SEAL_STORE_CPOL>;
 
+// EmitShiftLinesUni for a wave of ONE line class, the class fixed at compile time (round 5).
+// The generic emitter decides at every chunk, at run time, whether a line completes (its class),
+// whether the line is interior (fast store path) and which rows spill into the next line.  Each of
+// those branches splits the seal's pair loop into separate basic blocks, and at the join after a
+// flush whose store count differs per path the compiler can only wait vmcnt(0): the next block's
+// first load wait then also waits for the 8 line stores just issued (class-A waves flush in the
+// middle of the pair).  Here a wave of class PAR_ODD = 1 (d < 64) completes line q / 2 after every
+// odd chunk q, a wave of class 0 (d >= 64) after every even chunk, with no run-time test:
+//  - emit_steady(q, D) is the pair loop's emit (q >= 2, a full chunk): byte-address chunk writes,
+//    then at its parity the fast whole-line flush and an unconditional row shift.  Every line the
+//    pair loop completes is whole inside every output of the wave (the chunk that completes it is a
+//    full block); the one exception is line 1 of a class-0 output with d > 96, which holds tag
+//    bytes [128 - d, 32): it leaves with the zeros chunk 0 put there, and tag() writes the tag
+//    after a vmcnt(0) wait, so the tag lands after that line;
+//  - everything else (chunks 0 and 1 with line 0, the tail, the last line) takes the generic
+//    emitter's paths.
+// Shifting every row is harmless: the bytes moved past a row's carry are overwritten by the next
+// chunk before the next flush reads them.
+template <int PAR_ODD, int CP>
+struct EmitShiftLinesUniClassT : EmitShiftLinesT<true, CP> {
+    using Base = EmitShiftLinesT<true, CP>;
+    __device__ __forceinline__ void emit_steady(u32 q, const u32 D[16])
+    {
+        const u32 pos = (((u32)(uintptr_t)this->mine & 127u) + 64u * q) & 127u;
+        uint8_t *row0 = this->rows + this->lane * SROW + SHEAD;
+#pragma unroll
+        for (u32 c = 0; c < 4; c++)
+            *reinterpret_cast<v4u_ua *>(row0 + pos + 16u * c) = v4u_t{D[4 * c], D[4 * c + 1], D[4 * c + 2], D[4 * c + 3]};
+        this->last_q = q;
+        if ((q & 1u) != (u32)PAR_ODD)
+            return;
+        const u32 c = this->lane & 7u, r = this->lane >> 3;
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // the other lanes' ds_writes of this line
+        const u64 lb = this->ubase + (u32)__builtin_amdgcn_readfirstlane(128u * (q >> 1));
+#pragma unroll
+        for (u32 j = 0; j < 8; j++) {
+            const u32 F = 8u * j + r;
+            const uint4 v = *reinterpret_cast<const uint4 *>(this->rows + F * SROW + SHEAD + 16u * c);
+            buf_store16<CP>(lb, this->loff[j], v);
+        }
+        asm volatile("" ::: "memory");
+        uint4 *row = reinterpret_cast<uint4 *>(row0);
+        uint4 t[4];
+#pragma unroll
+        for (u32 u = 0; u < 4; u++)
+            t[u] = row[8u + u];
+#pragma unroll
+        for (u32 u = 0; u < 4; u++)
+            row[u] = t[u];
+        asm volatile("" ::: "memory");
+    }
+    __device__ __forceinline__ void tag(const u32 t[4])
+    {
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // every line store of the wave has landed
+        Base::tag(t);
+    }
+};
+template <int PAR_ODD>
+using EmitShiftLinesUniClassSeal = EmitShiftLinesUniClassT<PAR_ODD, CZ_SEAL_STORE_CPOL>;
+
+// the pair loops' emit: emitters that have a steady-state form (emit_steady) take it
+template <class EM, class = void>
+struct has_emit_steady : std::false_type {};
+template <class EM>
+struct has_emit_steady<EM, std::void_t<decltype(&EM::emit_steady)>> : std::true_type {};
+template <class EM>
+__device__ __forceinline__ void emit_steady(EM &em, u32 q, const u32 D[16])
+{
+    if constexpr (has_emit_steady<EM>::value)
+        em.emit_steady(q, D);
+    else
+        em.emit_full(q, D);
+}
+
 // Line staging for a wave of segments at arbitrary 16-byte aligned bases.  Like
 // EmitLines, 8 lanes write one 128-byte output line per store instruction, but
 // each frame's base and byte count are fetched from its owner lane with
@@ -2354,7 +2443,18 @@ __device__ __forceinline__ void seal_uniform_body(const uint8_t *__restrict__ in
                                  mlen, 0u, 0u};
             em.init(true);
             em.init_uniform(i - blockIdx.x * BLOCK, (u32)out_stride, out + (uint64_t)blockIdx.x * BLOCK * out_stride);
-            if (un0)
+            if (un0 && !em.mixed) {
+                // one line class per wave (class_permute): the class-static emitter
+                if (__builtin_amdgcn_readfirstlane((((u32)(uintptr_t)dst & 64u) == 0u) ? 1u : 0u)) {
+                    EmitShiftLinesUniClassSeal<1> ec{em};
+                    seal_frame<MODE, true, EmitShiftLinesUniClassSeal<1>, PAIR, true, true, INA>(src, len, fl,
+                                                                                               counter0 + i, key, ec);
+                } else {
+                    EmitShiftLinesUniClassSeal<0> ec{em};
+                    seal_frame<MODE, true, EmitShiftLinesUniClassSeal<0>, PAIR, true, true, INA>(src, len, fl,
+                                                                                               counter0 + i, key, ec);
+                }
+            } else if (un0)
                 seal_frame<MODE, true, EmitShiftLinesUniSeal, PAIR, true, true, INA>(src, len, fl, counter0 + i, key, em);
             else
                 seal_frame<MODE, true, EmitShiftLinesUniSeal, PAIR, false, true, INA>(src, len, fl, counter0 + i, key, em);
@@ -2411,6 +2511,7 @@ __global__ __launch_bounds__(BLOCK) CZ_OCC CZ_OPEN_UNI_OCC void k_seal_uniform_i
                                                allow_un0);
 }
 
+#if CZ_KPART_HAS(3)
 __global__ __launch_bounds__(BLOCK) void k_seal_desc(const cz_frame_desc *__restrict__ desc,
                                                       const uint32_t *__restrict__ order, uint32_t count,
                                                       const uint8_t *__restrict__ in, uint8_t *__restrict__ out,
@@ -2472,6 +2573,8 @@ __global__ __launch_bounds__(BLOCK) void k_open_desc(const cz_frame_desc *__rest
     if (nonces)
         nonces[i] = nonce;
 }
+
+#endif  // CZ_KPART_HAS(3)
 
 // Uniform open of one connection's bodies in order: frame i must beat frame
 // i-1's nonce, frame 0 must beat floor0 (when check != 0).
@@ -2632,6 +2735,7 @@ __global__ __launch_bounds__(BLOCK) CZ_OPEN_CARRY_OCC void k_open_uniform_carry(
     status[i] = (uint16_t)(st | (st == CZ_STATUS_OK ? (fl << 8) : 0u));
 }
 
+#if CZ_KPART_HAS(3)
 // ---- segmented (ragged) batches ------------------------------------------
 constexpr int SEGMODE_LINES = 1;  // line-staged stores for waves of equal-length segments
 constexpr int SEGMODE_PAIR = 2;   // whole-line input loads (seal)
@@ -3299,6 +3403,8 @@ __global__ __launch_bounds__(BLOCK) void k_copy16(uint4 *__restrict__ dst, const
     }
 }
 
+#endif  // CZ_KPART_HAS(3)
+
 // Staging choice for a uniform batch (all pointers 16-byte aligned assumed by the caller check).
 int pick_staging(uint64_t stride, uint32_t out_bytes, bool aligned)
 {
@@ -3314,24 +3420,40 @@ int pick_staging(uint64_t stride, uint32_t out_bytes, bool aligned)
 
 }  // namespace
 
-// run-time tuning knobs (cz_tune): whole-line input loads for the uniform kernels
-static int g_pair = 1;
-static int g_un0 = 1;  // scalar first Salsa round when the high nonce word is wave-uniform
-static int g_seglines = 1;  // line-staged stores for waves of equal-length segments
-static int g_shift = 1;     // uniform seal: shifted line staging for bodies at any byte offset
-static int g_open_ina = 1;  // uniform open: line path for bodies off 16-byte alignment (dword-aligned loads)
-static int g_seal_ina = 1;  // seal: staged / line paths for payloads off 16-byte alignment
+// run-time tuning knobs (one definition, in part 3; hidden: not part of the library's ABI)
+namespace czk_knobs {
+#define CZ_KNOB __attribute__((visibility("hidden")))
+#if CZ_KPART_HAS(3)
+// g_pair: whole-line input loads for the uniform kernels
+CZ_KNOB int g_pair = 1;
+CZ_KNOB int g_un0 = 1;  // scalar first Salsa round when the high nonce word is wave-uniform
+CZ_KNOB int g_seglines = 1;  // line-staged stores for waves of equal-length segments
+CZ_KNOB int g_shift = 1;     // uniform seal: shifted line staging for bodies at any byte offset
+CZ_KNOB int g_open_ina = 1;  // uniform open: line path for bodies off 16-byte alignment (dword-aligned loads)
+CZ_KNOB int g_seal_ina = 1;  // seal: staged / line paths for payloads off 16-byte alignment
 #ifndef CZ_OPEN_CARRY_DEFAULT
 #define CZ_OPEN_CARRY_DEFAULT 1
 #endif
-static int g_open_carry = CZ_OPEN_CARRY_DEFAULT;  // uniform open off 16-byte alignment: phase-sorted waves, carried lines
+CZ_KNOB int g_open_carry = CZ_OPEN_CARRY_DEFAULT;  // uniform open off 16-byte alignment: phase-sorted waves, carried lines
 // segment kernels: waves of 16-byte aligned outputs that are not all on 128-byte lines go through
 // EmitShiftLines (whole cache lines) instead of EmitSegLines (128-byte groups at each output's
 // base, two partial cache lines per group): Zipf seal with 16-byte output slots 1250 -> 1629 GiB/s
 #ifndef CZ_SHIFT16_DEFAULT
 #define CZ_SHIFT16_DEFAULT 1
 #endif
-static int g_shift16 = CZ_SHIFT16_DEFAULT;
+CZ_KNOB int g_shift16 = CZ_SHIFT16_DEFAULT;
+#else
+extern CZ_KNOB int g_pair;
+extern CZ_KNOB int g_un0;
+extern CZ_KNOB int g_seglines;
+extern CZ_KNOB int g_shift;
+extern CZ_KNOB int g_open_ina;
+extern CZ_KNOB int g_seal_ina;
+extern CZ_KNOB int g_open_carry;
+extern CZ_KNOB int g_shift16;
+#endif
+}  // namespace czk_knobs
+using namespace czk_knobs;
 
 // ---------------------------------------------------------------------------
 // Launchers (called from cz_host.cpp).  No allocation, no synchronisation:
@@ -3339,6 +3461,7 @@ static int g_shift16 = CZ_SHIFT16_DEFAULT;
 // ---------------------------------------------------------------------------
 extern "C" {
 
+#if CZ_KPART_HAS(1)
 hipError_t czk_seal_uniform(const void *in, uint64_t in_stride, void *out, uint64_t out_stride, uint32_t count,
                             uint32_t len, const void *subkey, uint64_t counter0, const uint8_t *flags8,
                             hipStream_t s)
@@ -3427,6 +3550,9 @@ hipError_t czk_seal_uniform_box(const void *in, uint64_t in_stride, void *out, u
     return hipGetLastError();
 }
 
+#endif  // CZ_KPART_HAS(1)
+
+#if CZ_KPART_HAS(3)
 hipError_t czk_seal_desc(const cz_frame_desc *desc, const uint32_t *order, uint32_t count, const void *in, void *out,
                          const void *subkeys, hipStream_t s)
 {
@@ -3449,6 +3575,9 @@ hipError_t czk_open_desc(const cz_frame_desc *desc, const uint32_t *order, uint3
     return hipGetLastError();
 }
 
+#endif  // CZ_KPART_HAS(3)
+
+#if CZ_KPART_HAS(2)
 hipError_t czk_open_uniform(const void *in, uint64_t in_stride, void *out, uint64_t out_stride, uint32_t count,
                             uint32_t size, const void *subkey, uint64_t floor0, int check, uint16_t *status,
                             hipStream_t s)
@@ -3565,6 +3694,9 @@ hipError_t czk_open_uniform(const void *in, uint64_t in_stride, void *out, uint6
     return hipGetLastError();
 }
 
+#endif  // CZ_KPART_HAS(2)
+
+#if CZ_KPART_HAS(3)
 uint32_t czk_nacl_one_limit(void);
 
 hipError_t czk_nacl_one(void *st, uint32_t len, int open, void *subcache, int miss, uint32_t out_off,
@@ -3718,5 +3850,7 @@ hipError_t czk_fill(void *buf, uint64_t nbytes, uint64_t seed, hipStream_t s)
     hipLaunchKernelGGL(k_fill, grid, dim3(BLOCK), 0, s, (uint8_t *)buf, nbytes, seed);
     return hipGetLastError();
 }
+
+#endif  // CZ_KPART_HAS(3)
 
 }  // extern "C"

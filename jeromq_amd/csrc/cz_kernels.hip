@@ -1411,9 +1411,8 @@ __device__ __forceinline__ u64 read_be64(const uint8_t *p)
 // the same chunk count can share the cooperative line emitter below.
 // ---------------------------------------------------------------------------
 
-// bytes [a, b) of unit v at global address p (st_range16 for a global pointer); out of line:
-// only an output's edge units take it
-__device__ __noinline__ void st_range16_g(u64 p, uint4 v, u32 a, u32 b)
+// bytes [a, b) of unit v at global address p (st_range16 for a global pointer)
+__device__ __forceinline__ void st_range16_g(u64 p, uint4 v, u32 a, u32 b)
 {
     if (b <= a)
         return;
@@ -1450,14 +1449,20 @@ __device__ __noinline__ void st_range16_g(u64 p, uint4 v, u32 a, u32 b)
         *reinterpret_cast<g_u8 *>(q) = (uint8_t)lo;
 }
 
-// unit v at global address p clipped to its bytes [a, b), minus [t0, t1) when t1 > t0
+// unit v at global address p clipped to its bytes [a, b), minus [t0, t1) when t1 > t0.  Out of
+// line (only an output's edge units take it), and one call per unit: the range store is inlined
+// once, run for the part below the hole and then for the part above it.
 __device__ __noinline__ void st_unit_clip(u64 p, uint4 v, u32 a, u32 b, u32 t0, u32 t1)
 {
-    if (t1 > t0) {
-        st_range16_g(p, v, a, b < t0 ? b : t0);
-        st_range16_g(p, v, a > t1 ? a : t1, b);
-    } else {
-        st_range16_g(p, v, a, b);
+    const bool hole = t1 > t0;
+    u32 lo = a, hi = hole && b > t0 ? t0 : b;
+#pragma nounroll
+    for (int part = 0; part < 2; part++) {
+        st_range16_g(p, v, lo, hi);
+        if (!hole)
+            break;
+        lo = a > t1 ? a : t1;
+        hi = b;
     }
 }
 
@@ -1480,10 +1485,9 @@ __device__ void zero_bytes(uint8_t *p, u32 n)
 // lines written piecewise), so lines are ABSOLUTE: lane L's output [mine, mine + total)
 // starts d = mine & 127 bytes into its first line.  Its LDS row holds the line being built
 // (bytes [0, 128)) plus up to 64 bytes of the next; chunk q lands at (d + 64q) & 127 with
-// aligned LDS writes: b128 / b64 when every offset in the wave is a multiple of 16 / 8,
-// else 17 dwords of the chunk funnel-shifted by d & 3 bytes in registers (the dword
-// straddling two chunks completed by the next one; ds_write_b128 at byte offsets stalled the
-// LDS, SQ_LDS_UNALIGNED_STALL 18% of wave cycles), and completes a line when it reaches byte 128: at even q for
+// b128 / b64 writes when every offset in the wave is a multiple of 16 / 8, else four
+// ds_write_b128 at the byte address (round 4; the dword funnel they replaced cost more VALU than
+// the LDS's unaligned splits cost time), and completes a line when it reaches byte 128: at even q for
 // "class A" outputs (d >= 64), at odd q for the others.  The wave then stores that line of 8
 // outputs per global_store_dwordx4 (8 lanes x 16 bytes; each output's base and byte count
 // come from its owner lane by ds_bpermute) and each completing lane moves its row's bytes
@@ -1496,6 +1500,9 @@ __device__ void zero_bytes(uint8_t *p, u32 n)
 constexpr u32 SROW = 208;  // 16 headroom + 192 bytes used; 52 dwords apart: conflict-free 16-lane b128
 constexpr u32 SHIFT_LDS_BYTES = 64 * SROW;  // EmitShiftLines: 13 KiB per wave
 constexpr u32 SHEAD = 16;  // row bytes before line-space byte 0 (a chunk's first dword may start 4 early)
+// the uniform seal's rows (EmitShiftLinesT WHOLE) + 16 bytes: the next body's header, written behind
+// an output's end at row byte <= 192, may run 16 bytes past the last row
+constexpr u32 SEAL_SHIFT_LDS_BYTES = WAVES * SHIFT_LDS_BYTES + 16u;
 // UNI (uniform batches: output i at out + i * stride): every lane fetches, once per frame, the
 // workgroup-relative frame index of the 8 outputs it stores for (ds_bpermute) and keeps their
 // 128-byte line offsets from the workgroup's line-aligned base in 8 VGPRs, so the interior-line
@@ -1523,7 +1530,14 @@ struct WaveRel {
     }
 };
 
-template <bool UNI, int CP = CZ_OPEN_STORE_CPOL>
+// WHOLE (the uniform seal, round 5): no unit of an output is written byte by byte.  The tag slot's
+// units (body bytes 16..31 and the header / ciphertext bytes that share their 16-byte units) are
+// skipped by the line flushes and written whole by tag() from the header, the tag and the first
+// ciphertext words kept since chunk 0.  Bodies back to back (out_stride == body length, the V2 wire
+// layout): an output's last unit is completed with the next body's first header bytes (its
+// "\x07MESSAGE" and nonce, known from the counter) and written whole, and the next output skips that
+// unit (init_ext).  Only the batch's first and last outputs keep a clipped edge unit.
+template <bool UNI, int CP = CZ_OPEN_STORE_CPOL, bool WHOLE = false>
 struct EmitShiftLinesT {
     static constexpr bool cooperative = true;
     uint8_t *rows;   // this wave's 64 rows of SROW bytes
@@ -1535,6 +1549,7 @@ struct EmitShiftLinesT {
     u64 ubase;       // UNI: the workgroup's first output address rounded down to 128 (wave-uniform)
     u32 loff[8];     // UNI: line offset from ubase of output F = 8j + lane / 8, plus 16 * (lane & 7)
     WaveRel wr;      // !UNI: 32-bit output offsets for the interior-line flush
+    u32 hw[6];       // WHOLE: this body's nonce words (body dwords 2, 3) and ciphertext dwords 8..11
 
     // UNI: rel = this lane's workgroup-relative frame index, wg_out = the workgroup's frame-0 output
     // (the launcher keeps 256 * stride + the output length below 2^31)
@@ -1554,19 +1569,30 @@ struct EmitShiftLinesT {
     }
 
     // the launchers keep d + total below 2^31
-    __device__ __forceinline__ void init(bool tag_slot)
+    // tag_whole (WHOLE): tag() will write the tag slot's units whole (the flushes skip them; they
+    // end by body byte 48, so the output must reach that far); otherwise a tag slot's bytes are
+    // clipped out of the line stores and the tag is stored over them.  (The same for the segment
+    // seal, tag-slot units whole where a frame is one segment, measured -1.4% / -0.7% / +0.5% on the
+    // Zipf 8-byte table / 1-byte offsets / 128-byte slots: not shipped)
+    __device__ __forceinline__ void init(bool tag_slot, bool tag_whole = false)
     {
         const u32 d = (u32)(uintptr_t)mine & 127u;
         walign = __builtin_amdgcn_ballot_w64((d & 15u) != 0u) == 0  ? 16u
                  : __builtin_amdgcn_ballot_w64((d & 7u) != 0u) == 0 ? 8u
                                                                      : 1u;
-        te = (d + total) | (tag_slot ? 0x80000000u : 0u);
+        te = (d + total) | (tag_slot ? 0x80000000u : 0u) | (WHOLE && tag_slot && tag_whole && total >= 48u ? 0x10000000u : 0u);
         const uint64_t a = __builtin_amdgcn_ballot_w64((((u32)(uintptr_t)mine) & 64u) != 0u);
         mixed = (a != 0 && ~a != 0) ? 1u : 0u;
         if constexpr (!UNI)
             wr.init(mine);
         else
             wr.ok = false;
+    }
+    // WHOLE, bodies back to back: ext_start -- the body before this one completes this output's
+    // first unit (skip it); ext_end -- complete the last unit with the next body's header
+    __device__ __forceinline__ void init_ext(bool ext_start, bool ext_end)
+    {
+        te |= (ext_start ? 0x40000000u : 0u) | (ext_end ? 0x20000000u : 0u);
     }
     // store, for every output F of the wave whose line completes now, its line k_F:
     // KIND FL_PHASE: a one-class wave after chunk q of its phase, every F's line k = q / 2;
@@ -1584,7 +1610,7 @@ struct EmitShiftLinesT {
             // Line k = q / 2 strictly inside every output of the wave (past the lines holding the
             // tag slot, whole before the output's end): unclipped stores, only the base fetched.
             const u32 k = q >> 1;
-            const bool inner = k >= 2u && 128u * (k + 1u) <= (te & 0x7fffffffu);
+            const bool inner = k >= 2u && 128u * (k + 1u) <= (te & 0x0fffffffu);
             if constexpr (UNI) {
                 if (__builtin_amdgcn_ballot_w64(!inner) == 0) {
                     const u64 lb = ubase + (u32)__builtin_amdgcn_readfirstlane(128u * k);
@@ -1633,7 +1659,7 @@ struct EmitShiftLinesT {
             const u32 bhi = (u32)__builtin_amdgcn_ds_bpermute(sel, (int)(u32)(mb >> 32));
             const u32 fe = (u32)__builtin_amdgcn_ds_bpermute(sel, (int)te);
             const u32 d = blo & 127u;           // output F's bytes are [d, e) of its line space
-            const u32 e = fe & 0x7fffffffu;
+            const u32 e = fe & 0x0fffffffu;
             u32 k;
             bool act = true;
             if constexpr (KIND == FL_PHASE) {
@@ -1650,11 +1676,16 @@ struct EmitShiftLinesT {
             const u64 p = ((((u64)bhi) << 32) | (blo & ~127u)) + u;
             // overlaps the tag slot, output bytes 16..31: u + 16 > d + 16 && u < d + 32 (lines 0 and 1 only)
             const bool tg = (KIND != FL_PHASE || q < 4u) && (fe >> 31) && u > d && u < d + 32u;
-            if (act && u >= d && u + 16u <= e && !tg) {
+            // WHOLE: units owned whole by a neighbour (ext) or by tag() are not this flush's
+            const u32 dd = (WHOLE && (fe & 0x40000000u)) ? (d + 15u) & ~15u : d;
+            const u32 ee = (WHOLE && (fe & 0x20000000u)) ? (e + 15u) & ~15u : e;
+            if (act && u >= dd && u + 16u <= ee && !tg) {
                 *reinterpret_cast<g_uint4 *>(p) = v4u_t{v.x, v.y, v.z, v.w};
-            } else if (act && u < e && u + 16u > d) {
+            } else if (WHOLE && tg && (fe & 0x10000000u)) {
+                // a unit of the tag slot: tag() writes it whole
+            } else if (act && u < ee && u + 16u > dd) {
                 // tag bytes [d + 16 - u, d + 32 - u) of this unit stay for tag()
-                st_unit_clip(p, v, d > u ? d - u : 0u, e < u + 16u ? e - u : 16u,
+                st_unit_clip(p, v, dd > u ? dd - u : 0u, ee < u + 16u ? ee - u : 16u,
                              tg ? (u < d + 16u ? d + 16u - u : 0u) : 0u,
                              tg ? (d + 32u - u < 16u ? d + 32u - u : 16u) : 0u);
             }
@@ -1697,6 +1728,19 @@ struct EmitShiftLinesT {
             for (u32 c = 0; c < 4; c++)
                 *reinterpret_cast<v4u_ua *>(row0 + pos + 16u * c) = v4u_t{D[4 * c], D[4 * c + 1], D[4 * c + 2], D[4 * c + 3]};
         }
+        if constexpr (WHOLE) {
+            if (q == 0u) {
+                hw[0] = D[2]; hw[1] = D[3];
+                hw[2] = D[8]; hw[3] = D[9]; hw[4] = D[10]; hw[5] = D[11];
+            }
+            // the chunk holding the output's end: the next body's header right behind it (its first
+            // bytes complete the last unit; the row has 16 bytes of slack past byte 192)
+            if ((te & 0x20000000u) && total > 64u * q && total <= 64u * q + 64u) {
+                const u64 nx = (((u64)bswap32(hw[0]) << 32) | (u64)bswap32(hw[1])) + 1u;
+                *reinterpret_cast<v4u_ua *>(row0 + pos + (total - 64u * q)) =
+                    v4u_t{HDR0, HDR1, bswap32((u32)(nx >> 32)), bswap32((u32)nx)};
+            }
+        }
         const bool done = (t & 64u) != 0u;
         if (mixed) {
             flush<FL_MIXED>(q);
@@ -1713,7 +1757,28 @@ struct EmitShiftLinesT {
     __device__ __forceinline__ void emit_full(u32 q, const u32 D[16]) { emit(q, D); }
     __device__ __forceinline__ void tag(const u32 t[4])
     {
-        reinterpret_cast<U16ua *>(mine + 16)->v = make_uint4(t[0], t[1], t[2], t[3]);
+        if (WHOLE && (te & 0x10000000u)) {
+            // the 16-byte units of the output that overlap its tag slot (body bytes 16..31), whole:
+            // unit A = body [s, s + 16) at pA = (mine + 16) rounded down to 16, s = pA - mine in
+            // 1..16, and for s < 16 unit B = body [s + 16, s + 32); from body dwords 0..11
+            const u32 H[12] = {HDR0, HDR1, hw[0], hw[1], t[0], t[1], t[2], t[3], hw[2], hw[3], hw[4], hw[5]};
+            uint8_t *pA = reinterpret_cast<uint8_t *>(((uintptr_t)mine + 16u) & ~(uintptr_t)15);
+            const u32 sft = (u32)(pA - mine), si = sft >> 2, sb = sft & 3u;
+            u32 Hs[9];
+#pragma unroll
+            for (int k = 0; k < 9; k++)
+                Hs[k] = si == 0u ? H[k] : si == 1u ? H[k + 1] : si == 2u ? H[k + 2] : si == 3u ? H[k + 3] : (k < 8 ? H[k + 4] : 0u);
+            u32 O[8];
+#pragma unroll
+            for (int k = 0; k < 8; k++)
+                O[k] = funnel(Hs[k + 1], Hs[k], sb);
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // after any line store that covered these units
+            *reinterpret_cast<uint4 *>(pA) = make_uint4(O[0], O[1], O[2], O[3]);
+            if (sft < 16u)
+                *reinterpret_cast<uint4 *>(pA + 16) = make_uint4(O[4], O[5], O[6], O[7]);
+        } else {
+            reinterpret_cast<U16ua *>(mine + 16)->v = make_uint4(t[0], t[1], t[2], t[3]);
+        }
     }
     __device__ __forceinline__ void finish()
     {
@@ -1738,7 +1803,7 @@ struct EmitShiftLinesT {
 using EmitShiftLines = EmitShiftLinesT<false>;
 using EmitShiftLinesUni = EmitShiftLinesT<true>;
 using EmitShiftLinesSeal = EmitShiftLinesT<false, CZ_SEAL_STORE_CPOL>;
-using EmitShiftLinesUniSeal = EmitShiftLinesT<true, CZ_SEAL_STORE_CPOL>;
+using EmitShiftLinesUniSeal = EmitShiftLinesT<true, CZ_SEAL_STORE_CPOL, true>;
 
 // EmitShiftLinesUni for a wave of ONE line class, the class fixed at compile time (round 5).
 // The generic emitter decides at every chunk, at run time, whether a line completes (its class),
@@ -1759,8 +1824,8 @@ using EmitShiftLinesUniSeal = EmitShiftLinesT<true, CZ_SEAL_STORE_CPOL>;
 // Shifting every row is harmless: the bytes moved past a row's carry are overwritten by the next
 // chunk before the next flush reads them.
 template <int PAR_ODD, int CP>
-struct EmitShiftLinesUniClassT : EmitShiftLinesT<true, CP> {
-    using Base = EmitShiftLinesT<true, CP>;
+struct EmitShiftLinesUniClassT : EmitShiftLinesT<true, CP, true> {
+    using Base = EmitShiftLinesT<true, CP, true>;
     __device__ __forceinline__ void emit_steady(u32 q, const u32 D[16])
     {
         const u32 pos = (((u32)(uintptr_t)this->mine & 127u) + 64u * q) & 127u;
@@ -2441,8 +2506,12 @@ __device__ __forceinline__ void seal_uniform_body(const uint8_t *__restrict__ in
             // bodies at any byte offset (dense packing, wire layout): byte-shifted line staging
             EmitShiftLinesUniSeal em{reinterpret_cast<uint8_t *>(smem) + (threadIdx.x >> 6) * SHIFT_LDS_BYTES, dst, lane,
                                  mlen, 0u, 0u};
-            em.init(true);
+            em.init(true, true);
             em.init_uniform(i - blockIdx.x * BLOCK, (u32)out_stride, out + (uint64_t)blockIdx.x * BLOCK * out_stride);
+            // bodies back to back (the V2 wire layout) whose last chunk is a tail chunk (emit, not
+            // the pair loop's emit_steady): edge units shared with the neighbours leave whole
+            const bool b2b = out_stride == (uint64_t)mlen && (mlen & 63u) != 0u;
+            em.init_ext(b2b && i > 0u, b2b && i + 1u < count);
             if (un0 && !em.mixed) {
                 // one line class per wave (class_permute): the class-static emitter
                 if (__builtin_amdgcn_readfirstlane((((u32)(uintptr_t)dst & 64u) == 0u) ? 1u : 0u)) {
@@ -3486,7 +3555,7 @@ hipError_t czk_seal_uniform(const void *in, uint64_t in_stride, void *out, uint6
     hipLaunchKernelGGL((k_seal_uniform_ina<ST, PR, INA>), grid, dim3(BLOCK), (LDS), s, (const uint8_t *)in,        \
                        in_stride, (uint8_t *)out, out_stride, count, len, (const uint8_t *)subkey, counter0,       \
                        flags8, g_un0)
-        const unsigned lds_l = WAVES * (LINE_LDS_BYTES + HOLD_LDS_BYTES), lds_s = WAVES * SHIFT_LDS_BYTES;
+        const unsigned lds_l = WAVES * (LINE_LDS_BYTES + HOLD_LDS_BYTES), lds_s = SEAL_SHIFT_LDS_BYTES;
         const unsigned lds_r = (unsigned)(WAVES * 64 * out_stride);
         if (so == ST_LINES) {
             if (i8) CZ_SEAL_LAUNCH_INA(ST_LINES, true, 8, lds_l);
@@ -3511,7 +3580,7 @@ hipError_t czk_seal_uniform(const void *in, uint64_t in_stride, void *out, uint6
     if (st == ST_DIRECT && in_al && len + 33u >= 256u && out_stride < (1ull << 22) && len < (1u << 29) && g_shift)
         st = ST_SHIFT;
     const unsigned lds = st == ST_LINES ? WAVES * (LINE_LDS_BYTES + HOLD_LDS_BYTES)
-                                        : st == ST_SHIFT ? WAVES * SHIFT_LDS_BYTES
+                                        : st == ST_SHIFT ? SEAL_SHIFT_LDS_BYTES
                                         : (st == ST_REGION ? (unsigned)(WAVES * 64 * out_stride) : 0u);
     // whole-line input pays for large frames (A/B: 4 KiB seal 2.34 vs 2.51 ms) but
     // not for the small frames of the region stager (100 B: 0.119 vs 0.114 ms)

@@ -1684,10 +1684,22 @@ struct EmitShiftLinesT {
             } else if (WHOLE && tg && (fe & 0x10000000u)) {
                 // a unit of the tag slot: tag() writes it whole
             } else if (act && u < ee && u + 16u > dd) {
-                // tag bytes [d + 16 - u, d + 32 - u) of this unit stay for tag()
-                st_unit_clip(p, v, dd > u ? dd - u : 0u, ee < u + 16u ? ee - u : 16u,
-                             tg ? (u < d + 16u ? d + 16u - u : 0u) : 0u,
-                             tg ? (d + 32u - u < 16u ? d + 32u - u : 16u) : 0u);
+                // bytes [a, b) of this unit, minus the tag bytes [t0, t1) that stay for tag()
+                const u32 a = dd > u ? dd - u : 0u, b = ee < u + 16u ? ee - u : 16u;
+                const u32 t0 = tg ? (u < d + 16u ? d + 16u - u : 0u) : 0u;
+                const u32 t1 = tg ? (d + 32u - u < 16u ? d + 32u - u : 16u) : 0u;
+                if (((a | b | t0 | t1) & 7u) == 0u) {
+                    // 8-byte boundaries (outputs on an 8-byte offset table): each half of the unit
+                    // is kept whole or not at all, one aligned 8-byte store per kept half
+                    const bool k0 = a == 0u && b >= 8u && !(t0 == 0u && t1 >= 8u);
+                    const bool k1 = a <= 8u && b == 16u && !(t0 <= 8u && t1 == 16u);
+                    if (k0)
+                        *reinterpret_cast<g_u64_ua *>(p) = ((u64)v.y << 32) | v.x;
+                    if (k1)
+                        *reinterpret_cast<g_u64_ua *>(p + 8u) = ((u64)v.w << 32) | v.z;
+                } else {
+                    st_unit_clip(p, v, a, b, t0, t1);
+                }
             }
         }
     }

@@ -1680,6 +1680,7 @@ struct EmitShiftLinesT {
             const u32 dd = (WHOLE && (fe & 0x40000000u)) ? (d + 15u) & ~15u : d;
             const u32 ee = (WHOLE && (fe & 0x20000000u)) ? (e + 15u) & ~15u : e;
             if (act && u >= dd && u + 16u <= ee && !tg) {
+                CZ_DIAG_STORE_GUARD(v)
                 *reinterpret_cast<g_uint4 *>(p) = v4u_t{v.x, v.y, v.z, v.w};
             } else if (WHOLE && tg && (fe & 0x10000000u)) {
                 // a unit of the tag slot: tag() writes it whole
@@ -1693,11 +1694,14 @@ struct EmitShiftLinesT {
                     // is kept whole or not at all, one aligned 8-byte store per kept half
                     const bool k0 = a == 0u && b >= 8u && !(t0 == 0u && t1 >= 8u);
                     const bool k1 = a <= 8u && b == 16u && !(t0 <= 8u && t1 == 16u);
+                    CZ_DIAG_STORE_GUARD(v)
                     if (k0)
                         *reinterpret_cast<g_u64_ua *>(p) = ((u64)v.y << 32) | v.x;
+                    CZ_DIAG_STORE_GUARD(v)
                     if (k1)
                         *reinterpret_cast<g_u64_ua *>(p + 8u) = ((u64)v.w << 32) | v.z;
                 } else {
+                    CZ_DIAG_STORE_GUARD(v)
                     st_unit_clip(p, v, a, b, t0, t1);
                 }
             }
@@ -1785,11 +1789,17 @@ struct EmitShiftLinesT {
             for (int k = 0; k < 8; k++)
                 O[k] = funnel(Hs[k + 1], Hs[k], sb);
             asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // after any line store that covered these units
-            *reinterpret_cast<uint4 *>(pA) = make_uint4(O[0], O[1], O[2], O[3]);
+            const uint4 oa = make_uint4(O[0], O[1], O[2], O[3]);
+            CZ_DIAG_STORE_GUARD(oa)
+            *reinterpret_cast<uint4 *>(pA) = oa;
+            const uint4 ob = make_uint4(O[4], O[5], O[6], O[7]);
+            CZ_DIAG_STORE_GUARD(ob)
             if (sft < 16u)
-                *reinterpret_cast<uint4 *>(pA + 16) = make_uint4(O[4], O[5], O[6], O[7]);
+                *reinterpret_cast<uint4 *>(pA + 16) = ob;
         } else {
-            reinterpret_cast<U16ua *>(mine + 16)->v = make_uint4(t[0], t[1], t[2], t[3]);
+            const uint4 tv = make_uint4(t[0], t[1], t[2], t[3]);
+            CZ_DIAG_STORE_GUARD(tv)
+            reinterpret_cast<U16ua *>(mine + 16)->v = tv;
         }
     }
     __device__ __forceinline__ void finish()
@@ -2570,7 +2580,7 @@ __device__ __forceinline__ void seal_uniform_body(const uint8_t *__restrict__ in
 }
 
 template <int ST, bool PAIR, int MODE = MODE_ZMQ>
-__global__ __launch_bounds__(BLOCK) CZ_OCC void k_seal_uniform(const uint8_t *__restrict__ in, uint64_t in_stride,
+__global__ __launch_bounds__(BLOCK) CZ_OCC CZ_OPEN_UNI_OCC void k_seal_uniform(const uint8_t *__restrict__ in, uint64_t in_stride,
                                                          uint8_t *__restrict__ out, uint64_t out_stride,
                                                          uint32_t count, uint32_t len,
                                                          const uint8_t *__restrict__ subkey, uint64_t counter0,

@@ -3,7 +3,8 @@
 Dense output is what the wire needs (bodies back to back, or behind V2 headers,
 V2Encoder.java:23-56): a 4 KiB body slot of 4129 bytes puts every frame at a
 different byte phase of the 128-byte line.  Cases:
-  * cz_seal_uniform at strides 4129 (dense), 4130, 4131, 4136, 4144 and 4226, at output
+  * cz_seal_uniform at strides 4129 (dense), 4130, 4131, 4136, 4144 and 4226, and bodies back to
+    back of 320 / 352 / 4033 / 333 / 1041 bytes (the round-5 whole-unit edges), at output
     bases shifted by 0..15 bytes, with a partial last wave: every body bit-exact against
     the oracle (CurveClientMechanism.encode -> Curve.afternm, Curve.java:129-137), and
     every byte between bodies left as the caller wrote it;
@@ -49,7 +50,10 @@ def _gaps_untouched(out, spans, lo, hi):
 
 
 @pytest.mark.parametrize("n,stride", [(4096, 4129), (4096, 4130), (4096, 4131), (4096, 4136), (4096, 4144),
-                                      (4096, 4226), (223, 256 + 5), (300, 333), (1000, 1041)])
+                                      (4096, 4226), (223, 256 + 5), (300, 333), (1000, 1041),
+                                      # bodies back to back whose length is a 64-byte multiple (no edge
+                                      # unit shared with the next body's header) or a 16-byte one
+                                      (287, 320), (319, 352), (4000, 4033)])
 @pytest.mark.parametrize("base", [0, 1, 8, 13])
 def test_seal_uniform_any_offset(torch_dev, subkeys, n, stride, base):
     torch, dev = torch_dev

@@ -219,3 +219,36 @@ def test_fuzz_uniform_vs_oracle(torch_dev, subkeys, L, seed):
     back = plain.cpu().numpy()
     for i in range(count):
         assert back[i * in_stride:i * in_stride + n].tobytes() == hin[i * in_stride:i * in_stride + n].tobytes()
+
+
+@pytest.mark.parametrize("seed", range(6))
+def test_fuzz_uniform_back_to_back_bodies(torch_dev, subkeys, seed):
+    """cz_seal_uniform with bodies back to back (out_stride == n + 33, the V2 wire layout) at a
+    random output base: the class-static, whole-unit emitter, whose edge
+    units carry the next body's header.  Body lengths near every residue that matters mod 64 and
+    mod 16, batches with partial workgroups and partial waves, counters crossing 2^32 inside a
+    wave; every body against the oracle and every byte around the batch untouched."""
+    torch, dev = torch_dev
+    from jeromq_amd import batch
+    rng = np.random.default_rng(7000 + seed)
+    mlen = 64 * int(rng.integers(4, 80)) + int(rng.choice([1, 15, 16, 17, 31, 32, 33, 47, 63]))
+    n = mlen - 33
+    count = int(rng.integers(300, 1300))
+    base = int(rng.integers(0, 16))
+    in_stride = (n + 15) // 16 * 16
+    c0 = [3, (1 << 32) - int(rng.integers(1, 600)), int(rng.integers(1, 1 << 40))][seed % 3]
+    hin = np.frombuffer(splitmix_bytes(in_stride * count, 7100 + seed), dtype=np.uint8).copy()
+    flags = rng.integers(0, 4, size=count).astype(np.uint8)
+    d_in = torch.from_numpy(hin).to(dev)
+    size = base + count * mlen + 64
+    d_buf = torch.full((size,), 0xA5, dtype=torch.uint8, device=dev)
+    batch.seal_uniform(d_in, in_stride, d_buf[base:], mlen, count, n, subkeys[0], c0,
+                       flags8=torch.from_numpy(flags).to(dev))
+    torch.cuda.synchronize()
+    out = d_buf.cpu().numpy()
+    for i in range(count):
+        o = base + i * mlen
+        want = or_curve_encode(hin[i * in_stride:i * in_stride + n].tobytes(), int(flags[i]), c0 + i, 0, PRECOMS[0])
+        assert out[o:o + mlen].tobytes() == want, f"frame {i} of {count} (body {mlen} B, base {base}, c0 {c0})"
+    assert not (out[:base] != 0xA5).any(), "bytes before the first body were written"
+    assert not (out[base + count * mlen:] != 0xA5).any(), "bytes past the last body were written"

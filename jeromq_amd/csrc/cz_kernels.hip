@@ -2454,20 +2454,43 @@ __device__ __forceinline__ u32 open_segment(const uint8_t *__restrict__ in, u32 
 }
 
 // Join a frame's segment records: H = Horner over segments with multipliers r^m.
+// The planner cuts every segment but a frame's last to the same length, so a lane needs two
+// powers, r^m_mid and r^m_last. One square-and-multiply chain over the bits yields both, its
+// loop bound wave-uniform; a multiply runs where any lane of the wave has that bit set. (Caching
+// r^m at each change of m instead ran one divergent exponentiation per distinct segment count
+// in the wave: ~45 us per Zipf batch, one latency-bound lane per split frame.) A middle segment
+// of another length, which no plan makes, still gets its own power.
 __device__ __forceinline__ void combine_tag(const u32 *__restrict__ R0, u32 nseg, u32 tag[4])
 {
     const F26 r = f26_from32(R0[8], R0[9], R0[10], R0[11], 0u);
     F26 H = f26_from32(R0[0], R0[1], R0[2], R0[3], R0[4]);
-    u32 cached_m = 0;
-    F26 cached;
-    for (u32 s = 1; s < nseg; s++) {
-        const u32 *R = R0 + 16u * s;
-        const u32 m = R[5];
-        if (m != cached_m) {
-            cached = f26_pow(r, m);
-            cached_m = m;
+    if (nseg > 1u) {
+        const u32 *RL = R0 + 16u * (nseg - 1u);
+        const u32 m_last = RL[5];
+        const u32 m_mid = nseg > 2u ? R0[16 + 5] : m_last;
+        const F26 hl = f26_from32(RL[0], RL[1], RL[2], RL[3], RL[4]);
+        F26 hn = nseg > 2u ? f26_from32(R0[16], R0[17], R0[18], R0[19], R0[20]) : hl;
+        F26 base = r, pm = {{1u, 0u, 0u, 0u, 0u}}, pl = pm;
+        for (u32 bit = 0; __builtin_amdgcn_ballot_w64(((m_mid | m_last) >> bit) != 0u) != 0; bit++) {
+            if (bit)
+                base = f26_mul(base, base);
+            if ((m_mid >> bit) & 1u)
+                pm = f26_mul(pm, base);
+            if ((m_last >> bit) & 1u)
+                pl = f26_mul(pl, base);
         }
-        H = f26_add(f26_mul(H, cached), f26_from32(R[0], R[1], R[2], R[3], R[4]));
+        for (u32 s = 1; s + 1u < nseg; s++) {
+            const u32 *R = R0 + 16u * s;
+            const F26 h = hn;
+            const u32 m = R[5];
+            if (s + 2u < nseg)  // next record's loads in flight under this multiply
+                hn = f26_from32(R[16], R[17], R[18], R[19], R[20]);
+            F26 pw = pm;
+            if (m != m_mid)
+                pw = f26_pow(r, m);
+            H = f26_add(f26_mul(H, pw), h);
+        }
+        H = f26_add(f26_mul(H, pl), hl);
     }
     Poly Q;
     f26_to32(H, Q.h0, Q.h1, Q.h2, Q.h3, Q.h4);

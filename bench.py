@@ -208,7 +208,7 @@ class Workload:
     """Builds one rank's device-resident batch and the per-step launch."""
 
     def __init__(self, cfg, frames, rank, dev, out_align=128, seg_blocks=128, in_align=64, plain_stride=0,
-                 in_stride=0, out_stride=0):
+                 in_stride=0, out_stride=0, fixed_len=0):
         self.cfg = cfg
         self.dev = dev
         key = torch.tensor(list(PRECOM), dtype=torch.uint8, device=dev).view(1, 32)
@@ -272,6 +272,8 @@ class Workload:
                 z = rng.zipf(1.2, size=frames)
                 j = np.concatenate([j, z[z <= 1024]])
             lens = (64 * j[:frames]).astype(np.uint64)
+            if fixed_len:  # diagnostic (tools/ab_cfg.py --fixed-len): the segment path on uniform frames
+                lens[:] = fixed_len
             desc = np.zeros(frames, dtype=batch.DESC_DTYPE)
             ia = np.uint64(in_align)
             in_len = (lens + ia - np.uint64(1)) // ia * ia

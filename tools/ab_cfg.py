@@ -35,13 +35,14 @@ def make(spec, frames, dev):
     ap.add_argument("--in-align", type=int, default=64)
     ap.add_argument("--out-align", type=int, default=128)
     ap.add_argument("--seg-blocks", type=int, default=128)
+    ap.add_argument("--fixed-len", type=int, default=0, help="zipf configs: every frame this long")
     ap.add_argument("--tune", action="append", default=[])
     a = ap.parse_args(toks)
     tune = [(k, int(v)) for k, v in (t.split("=") for t in a.tune)]
     with tuned(tune):
         wl = bench.Workload(a.config, frames, 0, dev, out_align=a.out_align, seg_blocks=a.seg_blocks,
                             in_align=a.in_align, plain_stride=a.plain_stride, in_stride=a.in_stride,
-                            out_stride=a.out_stride)
+                            out_stride=a.out_stride, fixed_len=a.fixed_len)
     wl.tune = tune
     return wl
 

@@ -43,28 +43,34 @@ def main():
     ap.add_argument("--steps", type=int, default=5)
     ap.add_argument("--frames", type=int, default=bench.FRAMES)
     ap.add_argument("--no-verify", action="store_true", help="diagnostic builds (CZ_DIAG_*) write wrong bytes")
+    ap.add_argument("--own-plan", action="store_true",
+                    help="each build plans its own batch (segment order is the planner's: cz_plan_segments)")
     a = ap.parse_args()
     torch.cuda.set_device(0)
     dev = torch.device("cuda:0")
     libs = [load(p) for p in a.libs]
     s = torch.cuda.current_stream()
     for spec in a.spec or ["4k"]:
-        _lib._LIB = libs[0]
-        wl = make(spec, a.frames, dev)
-        for L in libs:
+        wls = []
+        for L in (libs if a.own_plan else libs[:1]):
             _lib._LIB = L
-            wl.step()
+            wls.append(make(spec, a.frames, dev))
+        pick = (lambda k: wls[k]) if a.own_plan else (lambda k: wls[0])
+        for k, L in enumerate(libs):
+            _lib._LIB = L
+            pick(k).step()
             if not a.no_verify:
-                wl.verify_sample()
+                pick(k).verify_sample()
         for _ in range(10):
-            for L in libs:
+            for k, L in enumerate(libs):
                 _lib._LIB = L
-                wl.step()
+                pick(k).step()
         torch.cuda.synchronize()
         times = [[] for _ in libs]
         for _ in range(a.rounds):
             for k, L in enumerate(libs):
                 _lib._LIB = L
+                wl = pick(k)
                 wl.step()
                 e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
                 e0.record(s)
@@ -81,7 +87,7 @@ def main():
             base = base or gib
             print(f"{spec:32s} {os.path.basename(path):28s} median {med:.4f} ms  min {t.min():.4f} ms  "
                   f"{gib:8.1f} GiB/s  x{gib / base:.4f}", flush=True)
-        del wl
+        del wl, wls
         torch.cuda.empty_cache()
     _lib._LIB = libs[0]
 

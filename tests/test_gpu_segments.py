@@ -454,3 +454,86 @@ def test_open_segments_8byte_packed_equal_lengths(torch_dev, subkeys, L):
         elif want[i] == L.CZ_STATUS_CRYPTO:
             assert not pout[o:o + n].any(), f"frame {i} leaked plaintext"
         assert nn[i] == int(desc[i]["counter"])
+
+
+def _uneven_plan(plan, rng, open_, min_b0):
+    """Re-split every split frame of `plan` at random cuts (2..6 segments of unequal length, the
+    first at block 0, every other at or above `min_b0`), renumbering the partial records: the
+    kernels take any partition, and the combine then joins unequal middle segments (its general
+    per-segment power of r) as well as unequal last ones."""
+    segs = plan.segments
+    parts = {}
+    for sg in segs:
+        if sg["part"] != 0xFFFFFFFF:
+            parts.setdefault(int(sg["frame"]), []).append(sg)
+    keep = [sg for sg in segs if sg["part"] == 0xFFFFFFFF]
+    new_segs, combs, npart = [], [], 0
+    for c in plan.combines:
+        f = int(c["frame"])
+        nblk = max(int(s["first_block"]) + int(s["nblocks"]) for s in parts[f])
+        lo = min_b0
+        if nblk - lo < 2:
+            cuts = []
+        else:
+            k = int(rng.integers(1, min(5, nblk - lo) + 1))
+            cuts = sorted(int(x) for x in rng.choice(np.arange(lo, nblk), size=k, replace=False))
+        edges = [0] + cuts + [nblk]
+        combs.append((f, npart, len(edges) - 1, 0))
+        for s in range(len(edges) - 1):
+            new_segs.append((f, edges[s], edges[s + 1] - edges[s], npart + s))
+        npart += len(edges) - 1
+    from jeromq_amd import batch
+    out = np.zeros(len(keep) + len(new_segs), dtype=batch.SEGMENT_DTYPE)
+    out[:len(keep)] = keep
+    out[len(keep):] = new_segs
+    plan.segments = out
+    plan.combines = np.array(combs, dtype=batch.COMBINE_DTYPE)
+    plan.nseg, plan.ncomb, plan.npart = len(out), len(combs), npart
+    return plan
+
+
+@pytest.mark.parametrize("seed", [1, 2])
+def test_seal_open_segments_uneven_custom_plans(torch_dev, subkeys, L, seed):
+    """Segment plans that cut long frames at random, unequal points (not the planner's equal
+    segments): seal against the oracle, then open (with tampered frames) through uneven plans."""
+    torch, dev = torch_dev
+    from jeromq_amd import batch
+    rng = np.random.default_rng(seed)
+    lens = _boundary_lengths(6) + [int(x) for x in rng.integers(500, 20000, size=300)]
+    desc, hin, ob = _pack(lens, shift=0, seed=90 + seed)
+    plan = _uneven_plan(batch.SegmentPlan(desc, open_=False, seg_blocks=6), rng, False, 1).to(dev)
+    assert plan.ncomb > 50
+    d_out = torch.zeros(ob, dtype=torch.uint8, device=dev)
+    batch.seal_segments(_dev(torch_dev, desc), plan, _dev(torch_dev, hin), d_out, subkeys, desc_np=desc)
+    torch.cuda.synchronize()
+    sealed = d_out.cpu().numpy()
+    assert np.array_equal(sealed, _oracle_seal(desc, hin, ob))
+    # open the sealed bodies through another uneven plan (open segments s >= 1 start at block >= 2)
+    odesc = np.zeros(len(lens), dtype=DESC_DTYPE)
+    po = 0
+    for i, n in enumerate(lens):
+        odesc[i] = (int(desc[i]["out_off"]), po, n + 33, int(desc[i]["key_idx"]), int(desc[i]["counter"]) - 1,
+                    0x100, -1)
+        po += (n + 15) // 16 * 16
+    body = sealed.copy()
+    want = [L.CZ_STATUS_OK] * len(lens)
+    big = [i for i, n in enumerate(lens) if n > 64 * 9]
+    for j, i in enumerate(rng.choice(big, size=24, replace=False)):
+        n = lens[i] + 33
+        body[int(odesc[i]["in_off"]) + [20, 70, n // 2, n - 1][j % 4]] ^= 0x10
+        want[i] = L.CZ_STATUS_CRYPTO
+    oplan = _uneven_plan(batch.SegmentPlan(odesc, open_=True, seg_blocks=6), rng, True, 2).to(dev)
+    d_plain = torch.full((po + 64,), 0xA5, dtype=torch.uint8, device=dev)
+    status = torch.full((len(lens),), -1, dtype=torch.int16, device=dev)
+    batch.open_segments(_dev(torch_dev, odesc), oplan, _dev(torch_dev, body), d_plain, subkeys, status,
+                        desc_np=odesc)
+    torch.cuda.synchronize()
+    st = status.cpu().numpy().view(np.uint16)
+    pout = d_plain.cpu().numpy()
+    assert list(st & 0xff) == want
+    for i, n in enumerate(lens):
+        o, oi = int(odesc[i]["out_off"]), int(desc[i]["in_off"])
+        if want[i] == L.CZ_STATUS_OK:
+            assert pout[o:o + n].tobytes() == hin[oi:oi + n].tobytes(), f"frame {i} len {n}"
+        else:
+            assert not pout[o:o + n].any(), f"frame {i} leaked plaintext"

@@ -183,7 +183,11 @@ int cz_plan_order(const cz_frame_desc *h_desc, uint32_t count, uint32_t *h_order
  * sorts segments longest first (by output chunks), and lists the split frames for
  * the combine step, which joins the per-segment Poly1305 partials with r^m powers.
  * d_work must hold 64 bytes per part (*npart from the planner).  Output contract as
- * cz_seal_batch / cz_open_batch (statuses, nonces, zeroed plaintext on a bad tag). */
+ * cz_seal_batch / cz_open_batch (statuses, nonces, zeroed plaintext on a bad tag).
+ * A caller may also build its own plan: the segments of a split frame cover its box blocks
+ * [0, nblk) contiguously, one or more blocks each (open: segments after the first start at
+ * block 2 or later), with consecutive part indices from the frame's part0, in any order in
+ * the list and of any lengths (tests/test_gpu_segments.py cuts frames at random points). */
 typedef struct cz_segment {
     uint32_t frame;       /* index into the descriptor array */
     uint32_t first_block; /* first 64-byte box block of the segment */

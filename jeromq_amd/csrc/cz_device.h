@@ -426,9 +426,11 @@ __device__ __forceinline__ F26 f26_add(const F26 &a, const F26 &b)
     return r;
 }
 
-// r^e for e >= 1 (square and multiply)
+// r^e (square and multiply; r^0 = 1)
 __device__ __forceinline__ F26 f26_pow(const F26 &r, u32 e)
 {
+    if (e == 0u)
+        return F26{{1u, 0u, 0u, 0u, 0u}};
     F26 acc = r, base = r;
     bool have = false;
     for (u32 bit = 0; e >> bit; bit++) {

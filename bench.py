@@ -11,10 +11,13 @@ frame MORE.  Payload bytes: counter-based SplitMix64, generated on device.
   python bench.py [--gpus N] [--steps K] [--warmup W] [--config 4k|100b|zipf|zipf_lane|open4k|e2e4k]
 
 N > 1 (torch.distributed.run, one rank per GPU): every rank seals its own 2^20
-frames (counters offset by rank * 2^20): no collective on the timed path ("weak").
-Rank 0 prints ONE JSON line.  `value` = payload GiB/s over all ranks.  The 4k line also
-carries `seal_open_verify` (configs[4]: seal, then open + tag-verify of the same frames, timed
-apart from `value`) and, at N > 1, `scatter_gather` (RCCL scatter -> seal -> gather).
+frames (counters offset by rank * 2^20): no collective on the timed path ("weak"); barriers and
+the max-over-ranks timing run on a gloo control group.  Rank 0 prints ONE JSON line.  `value` =
+payload GiB/s over all ranks.  The 4k line also carries `seal_open_verify` (configs[4]: seal, then
+open + tag-verify of the same frames, timed apart from `value`).  At N > 1 the RCCL scatter ->
+seal -> gather leg runs AFTER that line is out, under a watchdog; rank 0 prints its result on a
+`SCATTER_GATHER {...}` line (not a JSON line), which `python bench.py --gpus N` merges into the
+line it relays.
 """
 import argparse
 import ctypes
@@ -62,6 +65,8 @@ def parse():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-scatter", action="store_true",
                     help="N>1, 4k: skip the separately timed RCCL scatter -> seal -> gather leg")
+    ap.add_argument("--leg-deadline", type=float, default=LEG_DEADLINE_S,
+                    help="N>1: seconds the scatter/gather leg may take after the main line before the ranks exit")
     ap.add_argument("--no-verify", action="store_true",
                     help="skip the parity spot check (diagnostic builds with CZ_DIAG_* only)")
     ap.add_argument("--no-roundtrip", action="store_true",
@@ -79,35 +84,101 @@ def _free_port():
     return port
 
 
-def launch_ranks(gpus, argv, popen=None):
+# The N > 1 ranks print the weak-scaling line first (one JSON line, everything `value` needs), then
+# run the separately timed RCCL scatter -> seal -> gather leg, whose result rank 0 prints on a line
+# of its own behind this tag: not a JSON line, so a reader that takes the lines starting with "{"
+# still sees exactly one, and a hang or error in the leg cannot cost the scaling line.
+SG_TAG = "SCATTER_GATHER "
+LEG_DEADLINE_S = 240.0       # ranks: the leg's own watchdog (then the ranks exit 0, line already out)
+LAUNCH_LEG_DEADLINE_S = 300.0  # launcher: after the main line, the wait for the leg before it kills the ranks
+
+
+def _kill_group(p):
+    """End the child torch.distributed.run and its ranks: the process group started for it
+    (start_new_session), never a pattern.  SIGTERM, then SIGKILL after 10 s."""
+    import signal
+    try:
+        pg = os.getpgid(p.pid)
+    except (ProcessLookupError, AttributeError):
+        return
+    for sig, wait_s in ((signal.SIGTERM, 10.0), (signal.SIGKILL, 10.0)):
+        try:
+            os.killpg(pg, sig)
+        except ProcessLookupError:
+            return
+        try:
+            p.wait(timeout=wait_s)
+            return
+        except Exception:  # subprocess.TimeoutExpired
+            pass
+
+
+def launch_ranks(gpus, argv, popen=None, cmd=None, kill=None, leg_deadline_s=LAUNCH_LEG_DEADLINE_S):
     """`python bench.py --gpus N` with N > 1 and no launcher around it: start the N ranks as a CHILD
-    `torch.distributed.run` (one process per GPU, rendezvous on 127.0.0.1), relay rank 0's JSON
-    line and return the child's exit status.  This process never touches the GPU (torch.cuda stays
-    uninitialised, the library is not loaded) and never execs: the ranks are its children.  The
-    line is checked before it is relayed: exactly one JSON line, n_gpus == N, one per_rank entry per
-    rank; anything else is an error (exit 1), so a run that silently timed fewer GPUs cannot pass."""
+    `torch.distributed.run` (one process per GPU, rendezvous on 127.0.0.1, its own session so the
+    ranks can be ended as one process group), relay rank 0's JSON line and return an exit status.
+    This process never touches the GPU (torch.cuda stays uninitialised, the library is not loaded)
+    and never execs: the ranks are its children.
+
+    The main line is checked before it is relayed: exactly one JSON line, n_gpus == N, one per_rank
+    entry per rank, the slowest-rank roofline and the CPU baseline; anything else is an error (the
+    child's exit status, or 1), so a run that silently timed fewer GPUs cannot pass.  After the main
+    line the ranks run the RCCL scatter/gather leg: its SG_TAG line is merged into the relayed line
+    as "scatter_gather".  If the leg has not reported within leg_deadline_s of the main line, the
+    child's process group is killed and the main line goes out with scatter_gather = {"error": ...};
+    an error the leg reports, or a non-zero exit after a good main line, is recorded the same way.
+    popen / cmd / kill: stand-ins for tests."""
+    import queue
     import subprocess
-    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={gpus}",
-           "--master-addr", "127.0.0.1", "--master-port", str(_free_port()), os.path.abspath(__file__)] + list(argv)
+    import threading
+    if cmd is None:
+        cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={gpus}",
+               "--master-addr", "127.0.0.1", "--master-port", str(_free_port()), os.path.abspath(__file__)] + list(argv)
     env = dict(os.environ)
     env.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")  # dmabuf IPC: RCCL needs it on this pool
     print("launching: " + " ".join(cmd), file=sys.stderr, flush=True)
-    p = (popen or subprocess.Popen)(cmd, stdout=subprocess.PIPE, text=True, env=env, cwd=ROOT)
-    lines = []
-    for ln in p.stdout:   # ranks' other stdout goes to stderr; the JSON line is held for the check
-        if ln.startswith("{"):
+    p = (popen or subprocess.Popen)(cmd, stdout=subprocess.PIPE, text=True, env=env, cwd=ROOT,
+                                    start_new_session=True)
+    kill = kill or _kill_group
+    q = queue.Queue()
+
+    def reader():
+        for ln in p.stdout:
+            q.put(ln)
+        q.put(None)
+    threading.Thread(target=reader, daemon=True).start()
+    lines, sg, eof, deadline = [], None, False, None
+    while not eof:
+        timeout = None if deadline is None else max(deadline - time.monotonic(), 0.0)
+        try:
+            ln = q.get(timeout=timeout)
+        except queue.Empty:
+            break                       # the leg's deadline passed
+        if ln is None:
+            eof = True
+        elif ln.startswith("{"):        # ranks' other stdout goes to stderr; the JSON line is held for the check
             lines.append(ln.strip())
+            if deadline is None:
+                deadline = time.monotonic() + leg_deadline_s
+        elif ln.startswith(SG_TAG):
+            try:
+                sg = json.loads(ln[len(SG_TAG):])
+            except ValueError:
+                sg = {"error": "unparsable leg line: " + ln.strip()[:200]}
         else:
             sys.stderr.write(ln)
             sys.stderr.flush()
+    killed = False
+    if not eof:
+        print(f"ranks still running {leg_deadline_s:.0f} s after the main line: killing their process group",
+              file=sys.stderr, flush=True)
+        kill(p)
+        killed = True
     rc = p.wait()
     assert not torch.cuda.is_initialized(), "launcher process initialised the GPU"
-    if rc != 0:
-        print(f"bench ranks failed (exit {rc})", file=sys.stderr)
-        return rc
     if len(lines) != 1:
-        print(f"expected one JSON line from rank 0, got {len(lines)}", file=sys.stderr)
-        return 1
+        print(f"expected one JSON line from rank 0, got {len(lines)} (ranks exit {rc})", file=sys.stderr)
+        return rc if rc and not killed else 1
     line = json.loads(lines[0])
     per = line.get("per_rank") or []
     if line.get("n_gpus") != gpus or len(per) != gpus or sorted(r["rank"] for r in per) != list(range(gpus)):
@@ -123,6 +194,16 @@ def launch_ranks(gpus, argv, popen=None):
     if line.get("value") is not None and missing:
         print(f"rank line lacks {missing}", file=sys.stderr)
         return 1
+    pending = isinstance(line.get("scatter_gather"), dict) and line["scatter_gather"].get("pending")
+    if sg is not None:
+        line["scatter_gather"] = sg
+    elif killed:
+        line["scatter_gather"] = {"error": f"timeout: no result {leg_deadline_s:.0f} s after the main line; "
+                                           "ranks killed by the launcher"}
+    elif pending:
+        line["scatter_gather"] = {"error": f"ranks exited (status {rc}) without reporting the leg"}
+    if rc != 0:
+        line["ranks_exit_status"] = rc   # after a good main line: recorded, not fatal
     line["launcher"] = "bench.py --gpus: child torch.distributed.run"
     print(json.dumps(line), flush=True)
     return 0
@@ -156,17 +237,33 @@ def setup_dist(args):
                          "(CZ_DIST_BACKEND=gloo rehearses N ranks on one GPU)")
     if ndev and local >= ndev:  # gloo rehearsal of N ranks on fewer GPUs; identity on a full node
         local %= ndev
+    global DATA_BACKEND
     if world > 1:
         import torch.distributed as dist
         torch.cuda.set_device(local)
-        if backend == "nccl":
-            dist.init_process_group("nccl", device_id=torch.device(f"cuda:{local}"))
-        else:
-            dist.init_process_group(backend)
+        # The default group is the CONTROL plane: barriers, the max-over-ranks timing and the per-rank
+        # figures, all host scalars, on gloo.  The timed path has no collective (frames are
+        # independent), so the weak-scaling line never depends on RCCL.  RCCL ("nccl", over xGMI)
+        # carries the data of the scatter/gather leg only, in a group of its own made after the
+        # line is out (data_group).
+        dist.init_process_group("gloo")
         assert dist.get_world_size() == world
+        DATA_BACKEND = backend
     else:
         torch.cuda.set_device(0)
     return world, rank, local
+
+
+DATA_BACKEND = None  # N > 1: the scatter/gather leg's backend ("nccl" = RCCL; "gloo" in rehearsals)
+
+
+def data_group():
+    """The scatter/gather leg's process group: a new RCCL group (collective: every rank calls it),
+    or the default gloo group in a gloo rehearsal (CZ_DIST_BACKEND=gloo)."""
+    import torch.distributed as dist
+    if DATA_BACKEND == "nccl":
+        return dist.new_group(backend="nccl")
+    return None
 
 
 def barrier(world):
@@ -866,10 +963,12 @@ def valu_roofline(pmc, kernel_s):
 def scatter_leg(wl, world, rank, dev):
     """North-star data movement, timed separately: rank 0 holds the whole
     batch, RCCL-scatters each rank its shard over xGMI, every rank seals its shard, and the
-    bodies are gathered back to rank 0.  Never folded into `value`."""
+    bodies are gathered back to rank 0.  Never folded into `value`; run after the main line is
+    out (run_leg), the bytes on data_group() (RCCL), barriers and the verdict on the gloo default."""
     from jeromq_amd import shard
     import torch.distributed as dist
-    gloo = dist.get_backend() != "nccl"
+    group = data_group()
+    gloo = DATA_BACKEND != "nccl"
     n_in, n_out = wl.d_in.numel(), wl.d_out.numel()
     sdev = torch.device("cpu") if gloo else dev
     full_in = full_out = None
@@ -882,15 +981,15 @@ def scatter_leg(wl, world, rank, dev):
         if gloo:
             full_in = full_in.cpu()
     recv = torch.empty(n_in, dtype=torch.uint8, device=sdev)
-    t_sc = shard.timed(lambda: shard.scatter_shards(recv, full_in), world)
+    t_sc = shard.timed(lambda: shard.scatter_shards(recv, full_in, group=group), world)
     ok = torch.equal(recv.to(dev), wl.d_in)
     saved = wl.d_in
     wl.d_in = recv.to(dev) if gloo else recv
     t_seal = shard.timed(wl.step, world)
     wl.d_in = saved
     send = wl.d_out.cpu() if gloo else wl.d_out
-    t_ga = shard.timed(lambda: shard.gather_shards(send, full_out), world)
-    okt = torch.tensor([1.0 if ok else 0.0], dtype=torch.float64, device="cpu" if gloo else dev)
+    t_ga = shard.timed(lambda: shard.gather_shards(send, full_out, group=group), world)
+    okt = torch.tensor([1.0 if ok else 0.0], dtype=torch.float64)
     dist.all_reduce(okt, op=dist.ReduceOp.MIN)
     verified = okt.item() == 1.0
     if rank == 0:
@@ -906,7 +1005,7 @@ def scatter_leg(wl, world, rank, dev):
     moved_out = (world - 1) * n_in
     moved_back = (world - 1) * n_out
     total_payload = world * wl.payload_bytes
-    return {"backend": dist.get_backend(), "scatter_ms": round(t_sc * 1e3, 3), "seal_ms": round(t_seal * 1e3, 3),
+    return {"backend": "nccl (RCCL)" if not gloo else "gloo", "scatter_ms": round(t_sc * 1e3, 3), "seal_ms": round(t_seal * 1e3, 3),
             "gather_ms": round(t_ga * 1e3, 3),
             "scatter_GBps": round(moved_out / t_sc / 1e9, 2), "gather_GBps": round(moved_back / t_ga / 1e9, 2),
             "bytes_out_of_rank0": moved_out, "bytes_into_rank0": moved_back,
@@ -1014,9 +1113,7 @@ def main():
     pmc = load_pmc(pmc_key)
     traffic = pmc.get("hbm_bytes_per_launch")
 
-    sg = None
-    if world > 1 and args.config == "4k" and not args.no_scatter:
-        sg = scatter_leg(wl, world, rank, dev)
+    want_leg = world > 1 and args.config == "4k" and not args.no_scatter
 
     rtl = None
     if args.config == "4k" and not args.no_roundtrip:
@@ -1082,19 +1179,54 @@ def main():
         }
         if rtl is not None:
             line["seal_open_verify"] = rtl
-        if sg is not None:
-            line["scatter_gather"] = sg
+        if want_leg:  # run after this line is out; rank 0 prints its result on an SG_TAG line
+            line["scatter_gather"] = {"pending": True, "reported_on": SG_TAG.strip() + " line",
+                                      "deadline_s": args.leg_deadline}
         if per_rank is not None:
             import torch.distributed as dist
             assert len(per_rank) == world
             line["per_rank"] = per_rank
             line["dist"] = {"backend": dist.get_backend(), "world_size": world,
                             "gpus_visible": torch.cuda.device_count(),
-                            "rccl": dist.get_backend() == "nccl"}
+                            "control_plane": "gloo (barriers, max-over-ranks timing, per-rank figures)",
+                            "data_backend": DATA_BACKEND,
+                            "rccl": DATA_BACKEND == "nccl"}
         print(json.dumps(line), flush=True)
+    if want_leg:
+        res = run_leg(lambda: scatter_leg(wl, world, rank, dev), rank, args.leg_deadline)
+        if res.get("error"):
+            os._exit(0)  # a failed collective can leave the groups unusable: no teardown, the line is out
     if world > 1:
         import torch.distributed as dist
         dist.destroy_process_group()
+
+
+def run_leg(fn, rank, deadline_s):
+    """Run an optional leg after the main line: rank 0 prints its result (or error) on an SG_TAG
+    line.  A watchdog ends this rank (exit 0: the main line is already out) if the leg has not
+    returned within deadline_s -- an RCCL collective that never completes cannot be interrupted
+    from Python.  Every rank runs its own watchdog, so a hung peer cannot hold the others."""
+    import threading
+    done = threading.Event()
+
+    def report(res):
+        if rank == 0:
+            print(SG_TAG + json.dumps(res), flush=True)
+
+    def watchdog():
+        if not done.wait(deadline_s):
+            report({"error": f"timeout: the leg did not finish within {deadline_s:.0f} s"})
+            sys.stderr.write(f"rank {rank}: leg timed out after {deadline_s:.0f} s, exiting\n")
+            sys.stderr.flush()
+            os._exit(0)
+    threading.Thread(target=watchdog, daemon=True).start()
+    try:
+        res = fn()
+    except Exception as e:  # noqa: BLE001 -- any failure of the optional leg is reported, not fatal
+        res = {"error": f"{type(e).__name__}: {e}"[:500]}
+    done.set()
+    report(res)
+    return res
 
 
 if __name__ == "__main__":

@@ -342,6 +342,11 @@ void cz_engine_destroy(cz_engine *e);
 /* returns a connection id >= 0; cn_nonce / cn_peer_nonce as cz_mech_create */
 int cz_engine_add_conn(cz_engine *e, int as_server, const uint8_t precom[32], uint64_t cn_nonce,
                        uint64_t cn_peer_nonce);
+/* the connection is gone (StreamEngine unplug / error, StreamEngine.java:334-370,1116-1131): its
+ * queued messages are dropped from the next flush, its received bytes and last flush_in payloads
+ * are discarded, its subkeys are wiped, and its id is reused by a later cz_engine_add_conn.
+ * Every other call on the id fails with CZ_EINVAL until then. */
+int cz_engine_remove_conn(cz_engine *e, int conn);
 /* pinned payload buffer inside the arena (no copy at send); NULL when the arena is full */
 void *cz_engine_msg_alloc(cz_engine *e, uint32_t len);
 /* queue one Msg (payload from cz_engine_msg_alloc, or copied into the arena); CZ_ENOMEM when the

@@ -132,6 +132,7 @@ SIGNATURES = {
     "cz_engine_create": (_I, [ctypes.POINTER(_VP), _U64, _I]),
     "cz_engine_destroy": (None, [_VP]),
     "cz_engine_add_conn": (_I, [_VP, _I, _VP, _U64, _U64]),
+    "cz_engine_remove_conn": (_I, [_VP, _I]),
     "cz_engine_msg_alloc": (_VP, [_VP, _U32]),
     "cz_engine_send": (_I, [_VP, _I, _VP, _U32, _I]),
     "cz_engine_flush_out": (_I, [_VP]),

@@ -14,6 +14,12 @@
 #error "CZ_DIAG_NOSTORE_ALL writes wrong bytes: never in the product library (build with CZ_LIB_OUT=<A/B path>)"
 #endif
 
+// -DCZ_DIAG_CLOCK (round 6) stamps s_memtime / s_memrealtime per wave of k_seal_uniform into a
+// device array (cz_diag_clock_read): correct output, but an extra store per wave, so A/B builds only.
+#if defined(CZ_PRODUCT_BUILD) && defined(CZ_DIAG_CLOCK)
+#error "CZ_DIAG_CLOCK is a measurement build: never in the product library"
+#endif
+
 #ifdef CZ_DIAG_NOSTORE_ALL
 #define CZ_DIAG_STORE_GUARD(v) if ((v).x == 0x13579bdfu && (v).w == 0x2468ace0u)
 #else

@@ -172,6 +172,7 @@ struct Conn {
     std::vector<Run> runs;            // wire stream of the last flush_out: pieces of h_wire, in send order
     std::vector<uint8_t> gathered;    // contiguous copy for cz_engine_wire_out when runs > 1
     std::vector<uint32_t> in_msgs;    // indices into Engine::in_msgs of the last flush_in
+    bool removed = false;             // cz_engine_remove_conn: the id and its key slots await reuse
 };
 
 struct OutMsg {
@@ -215,6 +216,7 @@ struct cz_engine {
     static constexpr int PIPE = 3;
     hipStream_t ps[PIPE] = {nullptr, nullptr, nullptr};
     std::vector<Conn> conns;
+    std::vector<int> free_ids;  // removed connections, reused (with their subkey slots) by add_conn
     DevBuf subkeys;  // 32 B per (connection, direction)
     uint32_t nkeys = 0;
     // outbound
@@ -264,7 +266,7 @@ struct cz_engine {
 
     Conn *conn(int c)
     {
-        if (c < 0 || (size_t)c >= conns.size()) {
+        if (c < 0 || (size_t)c >= conns.size() || conns[(size_t)c].removed) {
             fail(CZ_EINVAL, "cz_engine: unknown connection %d", c);
             return nullptr;
         }
@@ -879,15 +881,17 @@ int cz_engine_add_conn(cz_engine *e, int as_server, const uint8_t precom[32], ui
     if (!e || !precom)
         return fail(CZ_EINVAL, "cz_engine_add_conn: null pointer");
     hipError_t he;
-    if ((he = hipSetDevice(e->device)) != hipSuccess || (he = e->grow_keys(e->nkeys + 2)) != hipSuccess)
+    // a removed connection's id and subkey slots first, else two new table slots
+    const bool reuse = !e->free_ids.empty();
+    if ((he = hipSetDevice(e->device)) != hipSuccess || (!reuse && (he = e->grow_keys(e->nkeys + 2)) != hipSuccess))
         return hip_fail(he, "cz_engine_add_conn");
     void *dk = nullptr;
     if ((he = hipMalloc(&dk, 32)) != hipSuccess)
         return hip_fail(he, "hipMalloc");
     Conn c;
     c.server = as_server != 0;
-    c.tx_key = e->nkeys;
-    c.rx_key = e->nkeys + 1;
+    c.tx_key = reuse ? e->conns[(size_t)e->free_ids.back()].tx_key : e->nkeys;
+    c.rx_key = reuse ? e->conns[(size_t)e->free_ids.back()].rx_key : e->nkeys + 1;
     c.nonce = cn_nonce;
     c.peer_nonce = cn_peer_nonce;
     uint8_t *table = (uint8_t *)e->subkeys.ptr;
@@ -901,9 +905,49 @@ int cz_engine_add_conn(cz_engine *e, int as_server, const uint8_t precom[32], ui
         return hip_fail(he, "cz_engine_add_conn: subkeys");
     }
     (void)hipFree(dk);
+    if (reuse) {
+        const int id = e->free_ids.back();
+        e->free_ids.pop_back();
+        e->conns[(size_t)id] = std::move(c);
+        return id;
+    }
     e->nkeys += 2;
     e->conns.push_back(std::move(c));
     return (int)e->conns.size() - 1;
+}
+
+// StreamEngine teardown (unplug / error, StreamEngine.java:334-370,1116-1131) of an attached
+// connection: its queued messages leave the next flush, its received bytes and the payloads of the
+// last flush_in are dropped, its subkeys are wiped on the device, and its id and key slots are
+// reused by the next cz_engine_add_conn -- a long-lived IO thread with connection churn keeps a
+// bounded engine.
+int cz_engine_remove_conn(cz_engine *e, int conn)
+{
+    if (!e)
+        return fail(CZ_EINVAL, "cz_engine_remove_conn: null pointer");
+    Conn *c = e->conn(conn);
+    if (!c)
+        return CZ_EINVAL;
+    hipError_t he;
+    uint8_t *table = (uint8_t *)e->subkeys.ptr;
+    if ((he = hipSetDevice(e->device)) != hipSuccess ||
+        (he = hipMemsetAsync(table + 32ull * c->tx_key, 0, 32, e->stream)) != hipSuccess ||
+        (he = hipMemsetAsync(table + 32ull * c->rx_key, 0, 32, e->stream)) != hipSuccess ||
+        (he = hipStreamSynchronize(e->stream)) != hipSuccess)
+        return hip_fail(he, "cz_engine_remove_conn");
+    e->pend.erase(std::remove_if(e->pend.begin(), e->pend.end(), [conn](const OutMsg &m) { return (int)m.conn == conn; }),
+                  e->pend.end());
+    if (c->rx.ptr) {
+        explicit_bzero(c->rx.ptr, c->rx_len);
+        e->rxpool.free_list.push_back(c->rx);
+    }
+    Conn dead;
+    dead.tx_key = c->tx_key;
+    dead.rx_key = c->rx_key;
+    dead.removed = true;
+    *c = std::move(dead);
+    e->free_ids.push_back(conn);
+    return CZ_OK;
 }
 
 void *cz_engine_msg_alloc(cz_engine *e, uint32_t len)

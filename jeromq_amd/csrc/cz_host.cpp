@@ -6,6 +6,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <atomic>
 #include <cstdio>
 #include <cstring>
 #include <mutex>
@@ -243,9 +244,13 @@ static int nacl_one_launch(uint8_t *dst, const uint8_t *src, uint64_t len, const
 // (bench.py --config nacl, "large_boxes"; profiles/r05/nacl_large_boxes.json): one launch / segments
 // seal 57 / 166 us at 96 KiB, 114 / 254 at 256 KiB, 380 / 471 at 1 MiB, 1330 / 1174 at 4 MiB.
 // cz_tune("nacl_one_max") moves the edge; the Mechanism mirror uses the same one.
-static uint64_t g_nacl_one_bytes = 2ull << 20;
+// written by cz_tune while IO threads read it: relaxed atomic (a knob, no ordering needed)
+static std::atomic<uint64_t> g_nacl_one_bytes{2ull << 20};
 
-uint64_t nacl_one_bytes() { return std::max<uint64_t>(g_nacl_one_bytes, czk_nacl_one_max()); }
+uint64_t nacl_one_bytes()
+{
+    return std::max<uint64_t>(g_nacl_one_bytes.load(std::memory_order_relaxed), czk_nacl_one_max());
+}
 
 // NaCl box/open of one message on the device.  A MESSAGE is the NaCl box of
 // 0^32 || flags || payload, so m[32] rides as the flags byte and m[33:] as the payload; for open
@@ -479,8 +484,9 @@ const char *cz_version(void) { return "curvezmq-mi355x 0.1 (gfx950)"; }
 int cz_tune(const char *key, int value)
 {
     if (key && strcmp(key, "nacl_one_max") == 0) {  // bytes; at least one pass of k_nacl_one
-        const int old = (int)g_nacl_one_bytes;
-        g_nacl_one_bytes = std::min<uint64_t>(std::max<int64_t>(value, 0), czk_nacl_one_limit());
+        const int old = (int)g_nacl_one_bytes.load(std::memory_order_relaxed);
+        g_nacl_one_bytes.store(std::min<uint64_t>(std::max<int64_t>(value, 0), czk_nacl_one_limit()),
+                               std::memory_order_relaxed);
         return old;
     }
     int old = czk_tune(key, value);

@@ -1503,6 +1503,12 @@ constexpr u32 SHEAD = 16;  // row bytes before line-space byte 0 (a chunk's firs
 // the uniform seal's rows (EmitShiftLinesT WHOLE) + 16 bytes: the next body's header, written behind
 // an output's end at row byte <= 192, may run 16 bytes past the last row
 constexpr u32 SEAL_SHIFT_LDS_BYTES = WAVES * SHIFT_LDS_BYTES + 16u;
+// EmitShiftLinesT keeps its flag bits 28..31 (tag_whole, ext_end, ext_start, tag slot) above the
+// output's end d + total in `te`, so the launchers send an output to ST_SHIFT only when
+// d + total < 2^28 with d < 128: total <= SHIFT_TOTAL_MAX.
+constexpr u32 SHIFT_TE_FLAG_BITS = 0xf0000000u;
+constexpr u32 SHIFT_TOTAL_MAX = (1u << 28) - 128u;
+static_assert(((SHIFT_TOTAL_MAX + 127u) & SHIFT_TE_FLAG_BITS) == 0u, "te's end field overlaps its flag bits");
 // UNI (uniform batches: output i at out + i * stride): every lane fetches, once per frame, the
 // workgroup-relative frame index of the 8 outputs it stores for (ds_bpermute) and keeps their
 // 128-byte line offsets from the workgroup's line-aligned base in 8 VGPRs, so the interior-line
@@ -1568,7 +1574,7 @@ struct EmitShiftLinesT {
         }
     }
 
-    // the launchers keep d + total below 2^31
+    // the launchers keep d + total below 2^28 (SHIFT_TOTAL_MAX): bits 28..31 of te are flags
     // tag_whole (WHOLE): tag() will write the tag slot's units whole (the flushes skip them; they
     // end by body byte 48, so the output must reach that far); otherwise a tag slot's bytes are
     // clipped out of the line stores and the tag is stored over them.  (The same for the segment
@@ -1610,7 +1616,7 @@ struct EmitShiftLinesT {
             // Line k = q / 2 strictly inside every output of the wave (past the lines holding the
             // tag slot, whole before the output's end): unclipped stores, only the base fetched.
             const u32 k = q >> 1;
-            const bool inner = k >= 2u && 128u * (k + 1u) <= (te & 0x0fffffffu);
+            const bool inner = k >= 2u && 128u * (k + 1u) <= (te & ~SHIFT_TE_FLAG_BITS);
             if constexpr (UNI) {
                 if (__builtin_amdgcn_ballot_w64(!inner) == 0) {
                     const u64 lb = ubase + (u32)__builtin_amdgcn_readfirstlane(128u * k);
@@ -1659,7 +1665,7 @@ struct EmitShiftLinesT {
             const u32 bhi = (u32)__builtin_amdgcn_ds_bpermute(sel, (int)(u32)(mb >> 32));
             const u32 fe = (u32)__builtin_amdgcn_ds_bpermute(sel, (int)te);
             const u32 d = blo & 127u;           // output F's bytes are [d, e) of its line space
-            const u32 e = fe & 0x0fffffffu;
+            const u32 e = fe & ~SHIFT_TE_FLAG_BITS;
             u32 k;
             bool act = true;
             if constexpr (KIND == FL_PHASE) {
@@ -2602,6 +2608,29 @@ __device__ __forceinline__ void seal_uniform_body(const uint8_t *__restrict__ in
             zero_bytes(dst + mlen, (u32)(out_stride - mlen));
 }
 
+#ifdef CZ_DIAG_CLOCK
+// Clock diagnostic (tools/build_variant.sh NAME -DCZ_DIAG_CLOCK, tools/clock_stamp.py): every wave of
+// k_seal_uniform stamps the shader clock counter (s_memtime) and the 100 MHz constant counter
+// (s_memrealtime) when it starts and when it leaves; lane 0 writes the four values with a vector
+// store.  Wave clock = d(memtime) / d(realtime) * 100 MHz, unprofiled.  Output bytes are unchanged.
+constexpr u32 DIAG_CLOCK_WAVES = 1u << 16;
+static __device__ uint64_t g_diag_clock[DIAG_CLOCK_WAVES * 4u];
+#define CZ_DIAG_CLOCK_BEGIN                                                                                   \
+    const uint64_t dc_t0 = __builtin_amdgcn_s_memtime(), dc_r0 = __builtin_amdgcn_s_memrealtime();
+#define CZ_DIAG_CLOCK_END                                                                                     \
+    {                                                                                                         \
+        const uint64_t dc_t1 = __builtin_amdgcn_s_memtime(), dc_r1 = __builtin_amdgcn_s_memrealtime();       \
+        const u32 w = blockIdx.x * WAVES + (threadIdx.x >> 6);                                                \
+        if ((threadIdx.x & 63u) == 0u && w < DIAG_CLOCK_WAVES) {                                              \
+            volatile uint64_t *g = g_diag_clock + 4u * w;                                                     \
+            g[0] = dc_t0; g[1] = dc_r0; g[2] = dc_t1; g[3] = dc_r1;                                           \
+        }                                                                                                     \
+    }
+#else
+#define CZ_DIAG_CLOCK_BEGIN
+#define CZ_DIAG_CLOCK_END
+#endif
+
 template <int ST, bool PAIR, int MODE = MODE_ZMQ>
 __global__ __launch_bounds__(BLOCK) CZ_OCC CZ_OPEN_UNI_OCC void k_seal_uniform(const uint8_t *__restrict__ in, uint64_t in_stride,
                                                          uint8_t *__restrict__ out, uint64_t out_stride,
@@ -2609,8 +2638,10 @@ __global__ __launch_bounds__(BLOCK) CZ_OCC CZ_OPEN_UNI_OCC void k_seal_uniform(c
                                                          const uint8_t *__restrict__ subkey, uint64_t counter0,
                                                          const uint8_t *__restrict__ flags8, int allow_un0)
 {
+    CZ_DIAG_CLOCK_BEGIN
     seal_uniform_body<ST, PAIR, MODE, 16>(in, in_stride, out, out_stride, count, len, subkey, counter0, flags8,
                                           allow_un0);
+    CZ_DIAG_CLOCK_END
 }
 
 // payloads off 16-byte alignment (INA 8 / 1): at least 3 waves per SIMD (uncapped, the funnelled
@@ -3593,7 +3624,7 @@ hipError_t czk_seal_uniform(const void *in, uint64_t in_stride, void *out, uint6
     if (!in_al && g_pair && g_seal_ina && len >= 64u) {
         const bool out_al = ((((uintptr_t)out | out_stride) & 15u) == 0);
         int so = pick_staging(out_stride, len + 33u, out_al);
-        if (so == ST_DIRECT && len + 33u >= 256u && out_stride < (1ull << 22) && len < (1u << 29) && g_shift)
+        if (so == ST_DIRECT && len + 33u >= 256u && out_stride < (1ull << 22) && len <= SHIFT_TOTAL_MAX - 33u && g_shift)
             so = ST_SHIFT;
         const bool i8 = (((uintptr_t)in | in_stride) & 7u) == 0;
 #define CZ_SEAL_LAUNCH_INA(ST, PR, INA, LDS)                                                                  \
@@ -3622,7 +3653,7 @@ hipError_t czk_seal_uniform(const void *in, uint64_t in_stride, void *out, uint6
     int st = pick_staging(out_stride, len + 33u, al);
     // bodies at any byte offset (dense slots, wire layout) from aligned payloads: shifted line staging
     // (EmitShiftLinesUni's buffer-store offsets, below 256 * stride + len + 160, stay below 2^31)
-    if (st == ST_DIRECT && in_al && len + 33u >= 256u && out_stride < (1ull << 22) && len < (1u << 29) && g_shift)
+    if (st == ST_DIRECT && in_al && len + 33u >= 256u && out_stride < (1ull << 22) && len <= SHIFT_TOTAL_MAX - 33u && g_shift)
         st = ST_SHIFT;
     const unsigned lds = st == ST_LINES ? WAVES * (LINE_LDS_BYTES + HOLD_LDS_BYTES)
                                         : st == ST_SHIFT ? SEAL_SHIFT_LDS_BYTES
@@ -3663,6 +3694,18 @@ hipError_t czk_seal_uniform_box(const void *in, uint64_t in_stride, void *out, u
                            g_un0);
     return hipGetLastError();
 }
+
+#ifdef CZ_DIAG_CLOCK
+// diagnostic builds only: copy the last k_seal_uniform launch's wave stamps (4 x u64 per wave) out
+extern "C" __attribute__((visibility("default"))) int cz_diag_clock_read(uint64_t *host, uint64_t waves)
+{
+    if (waves > DIAG_CLOCK_WAVES)
+        waves = DIAG_CLOCK_WAVES;
+    return hipMemcpyFromSymbol(host, HIP_SYMBOL(g_diag_clock), waves * 32u, 0, hipMemcpyDeviceToHost) == hipSuccess
+               ? (int)waves
+               : -1;
+}
+#endif
 
 #endif  // CZ_KPART_HAS(1)
 
@@ -3716,7 +3759,8 @@ hipError_t czk_open_uniform(const void *in, uint64_t in_stride, void *out, uint6
     int st_out = size >= 33u ? pick_staging(out_stride, nout, out_al) : (int)ST_DIRECT;
     // plaintext at any byte offset (slots that are not 128-byte multiples): byte-shifted line
     // staging, as the seal's bodies (EmitShiftLinesUni; its buffer-store offsets stay below 2^31)
-    if (st_out == ST_DIRECT && size >= 33u && nout >= 256u && out_stride < (1ull << 22) && g_shift)
+    if (st_out == ST_DIRECT && size >= 33u && nout >= 256u && nout <= SHIFT_TOTAL_MAX && out_stride < (1ull << 22) &&
+        g_shift)
         st_out = ST_SHIFT;
     const uint64_t ia = (uintptr_t)in | in_stride;
     const int ina = (ia & 15u) == 0 ? 16 : (ia & 7u) == 0 ? 8 : 1;

@@ -57,6 +57,11 @@ class CurveBatchEngine:
             _lib.check(rc, "cz_engine_add_conn")
         return rc
 
+    def remove_connection(self, conn):
+        """The connection is gone (StreamEngine teardown): queued messages and received bytes are
+        dropped, its subkeys wiped, and its id reused by a later add_connection."""
+        _lib.check(self._L.cz_engine_remove_conn(self._h, conn), "cz_engine_remove_conn")
+
     def msg_alloc(self, n):
         """Pinned payload buffer in the engine arena (ZMQ_MSG_ALLOCATOR); a ctypes array or None."""
         p = self._L.cz_engine_msg_alloc(self._h, n)

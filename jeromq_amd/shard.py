@@ -40,33 +40,35 @@ def balance_by_bytes(lens, world):
     return b
 
 
-def scatter_shards(shard, full=None, src=0):
+def scatter_shards(shard, full=None, src=0, group=None):
     """Rank `src` holds `full` (world * shard.numel() bytes, rank r's shard at r*shard.numel());
-    every rank receives its shard into `shard`.  Collective: every rank calls it."""
-    world = dist.get_world_size()
+    every rank receives its shard into `shard`.  Collective: every rank calls it.  group: the
+    process group that carries the bytes (an RCCL group for device tensors; None = the default)."""
+    world = dist.get_world_size(group)
     if dist.get_rank() == src:
         if full is None or full.numel() != world * shard.numel():
             raise ValueError("scatter_shards: full must hold world * shard bytes on the source rank")
         parts = list(full.view(world, -1).unbind(0))
-        dist.scatter(shard, scatter_list=parts, src=src)
+        dist.scatter(shard, scatter_list=parts, src=src, group=group)
     else:
-        dist.scatter(shard, src=src)
+        dist.scatter(shard, src=src, group=group)
 
 
-def gather_shards(shard, full=None, dst=0):
+def gather_shards(shard, full=None, dst=0, group=None):
     """Inverse of scatter_shards: rank `dst` receives every rank's shard into `full`."""
-    world = dist.get_world_size()
+    world = dist.get_world_size(group)
     if dist.get_rank() == dst:
         if full is None or full.numel() != world * shard.numel():
             raise ValueError("gather_shards: full must hold world * shard bytes on the destination rank")
         parts = list(full.view(world, -1).unbind(0))
-        dist.gather(shard, gather_list=parts, dst=dst)
+        dist.gather(shard, gather_list=parts, dst=dst, group=group)
     else:
-        dist.gather(shard, dst=dst)
+        dist.gather(shard, dst=dst, group=group)
 
 
 def timed(fn, world, device_sync=True):
-    """Run fn between barriers; return the slowest rank's wall time in seconds."""
+    """Run fn between barriers of the default group; return the slowest rank's wall time in
+    seconds (the reduction on the default group's device: host for gloo)."""
     import time
     dist.barrier()
     if device_sync and torch.cuda.is_available():

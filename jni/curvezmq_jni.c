@@ -12,9 +12,9 @@
  *
  * Contracts:
  *  - jnacl calls return jnacl's 0 / -1.  Every array is checked against the lengths the call
- *    reads or writes before anything else happens (a short array is -1, never an overrun).  Arrays
- *    are pinned with Get/ReleasePrimitiveArrayCritical around the one native call and nothing else:
- *    inputs are released with JNI_ABORT (never copied back), outputs with 0.
+ *    reads or writes before anything else happens (a short array is -1, never an overrun).  No
+ *    Java array is pinned while the library runs: inputs are copied into native staging
+ *    (GetByteArrayRegion), outputs copied back on success (SetByteArrayRegion), the staging wiped.
  *  - Batch and engine calls take direct ByteBuffers (pinned memory from hostAlloc / msgAlloc for
  *    full PCIe rate) and return the library's CZ_* codes; a buffer smaller than the call needs, or
  *    a non-direct buffer, is CZ_EINVAL before the library is entered.
@@ -24,6 +24,7 @@
  *       jni/curvezmq_jni.c -Ljeromq_amd -lcurvezmq_mi355x -o libcurvezmq_jni.so
  * Without a JDK (this image; the CPU tests): add -DCZ_JNI_MIN to compile against jni/jni_min.h.
  */
+#define _DEFAULT_SOURCE /* explicit_bzero */
 #ifdef CZ_JNI_MIN
 #include "jni_min.h"
 #else
@@ -31,57 +32,82 @@
 #endif
 #include <stdint.h>
 #include <stdlib.h>
+#include <string.h>
 
 #include "curvezmq_mi355x.h"
 
-/* ---- pinned primitive arrays ---------------------------------------------------------------- */
+/* ---- Java byte[] arguments: staged, never pinned across a library call ------------------------
+ * A library call is a GPU launch and a stream sync (~20 us).  Holding a Java array with
+ * GetPrimitiveArrayCritical across it would lock the GC out of every thread for that long, per
+ * CURVE message.  So the byte[] natives copy their inputs into this thread's native staging with
+ * GetByteArrayRegion, run the library on the staging, and on success copy the outputs back with
+ * SetByteArrayRegion (a failed call -- a bad tag -- leaves the output array untouched).  The copies
+ * are the ones the library makes into its pinned staging anyway, one level up.  The staging holds
+ * plaintext and keys, so it is wiped after every call. */
 
 typedef struct {
     jbyteArray a;
     jlong need; /* bytes the call touches */
-    int out;    /* written by the call: released with 0 (copy back), inputs with JNI_ABORT */
-    void *p;
-} crit_arg;
+    int out;    /* written by the call: copied back on success; inputs are only read */
+    uint8_t *p; /* the argument's place in the staging */
+} jarr_arg;
 
-/* Check every array's length first, then pin them in order; -1 (nothing pinned) on a null or short
- * array or a failed pin. */
-static int crit_acquire(JNIEnv *env, crit_arg *v, int n)
+static _Thread_local uint8_t *t_stage;
+static _Thread_local size_t t_stage_cap;
+
+static size_t stage_round(jlong need) { return ((size_t)need + 15u) & ~(size_t)15u; }
+
+/* Check every array's length first (-1 with nothing read on a null or short array), then give every
+ * argument its staging and copy the inputs in.  -1 if the staging cannot grow or the VM raised. */
+static int stage_in(JNIEnv *env, jarr_arg *v, int n, size_t *used)
 {
+    size_t total = 0;
+    *used = 0;
     for (int i = 0; i < n; i++) {
         v[i].p = NULL;
         if (!v[i].a || v[i].need < 0 || (jlong)(*env)->GetArrayLength(env, v[i].a) < v[i].need)
             return -1;
+        total += stage_round(v[i].need);
     }
-    for (int i = 0; i < n; i++) {
-        v[i].p = (*env)->GetPrimitiveArrayCritical(env, v[i].a, NULL);
-        if (!v[i].p) {
-            for (int j = i - 1; j >= 0; j--)
-                (*env)->ReleasePrimitiveArrayCritical(env, v[j].a, v[j].p, JNI_ABORT);
+    if (total > t_stage_cap) {
+        uint8_t *p = (uint8_t *)malloc(total);
+        if (!p)
             return -1;
+        if (t_stage) {
+            explicit_bzero(t_stage, t_stage_cap);
+            free(t_stage);
         }
+        t_stage = p;
+        t_stage_cap = total;
+    }
+    size_t off = 0;
+    for (int i = 0; i < n; i++) {
+        v[i].p = t_stage + off;
+        if (!v[i].out && v[i].need)
+            (*env)->GetByteArrayRegion(env, v[i].a, 0, (jsize)v[i].need, (jbyte *)v[i].p);
+        off += stage_round(v[i].need);
+    }
+    *used = off;
+    if ((*env)->ExceptionCheck(env)) {
+        explicit_bzero(t_stage, off);
+        return -1;
     }
     return 0;
 }
 
-static void crit_release(JNIEnv *env, crit_arg *v, int n)
+/* rc == 0: copy the outputs back; always: wipe the staging.  Returns rc. */
+static int stage_out(JNIEnv *env, jarr_arg *v, int n, size_t used, int rc)
 {
-    for (int i = n - 1; i >= 0; i--)
-        (*env)->ReleasePrimitiveArrayCritical(env, v[i].a, v[i].p, v[i].out ? 0 : JNI_ABORT);
+    if (rc == 0)
+        for (int i = 0; i < n; i++)
+            if (v[i].out && v[i].need)
+                (*env)->SetByteArrayRegion(env, v[i].a, 0, (jsize)v[i].need, (const jbyte *)v[i].p);
+    if (used)
+        explicit_bzero(t_stage, used);
+    return rc;
 }
 
-#define U8(i) ((uint8_t *)v[i].p)
-
-/* The library creates a thread's single-shot context (HIP stream, device buffers, pinned staging)
- * on its first call.  Do that before the first pin of each thread, so HIP runtime initialisation
- * never runs inside a critical region (the GC is locked out while arrays are pinned).  A failure
- * (no GPU) is left to the call itself, which then returns -1. */
-static _Thread_local int t_warm;
-
-static void warm_thread(void)
-{
-    if (!t_warm && cz_nacl_thread_init() == CZ_OK)
-        t_warm = 1;
-}
+#define U8(i) (v[i].p)
 
 /* ---- com.neilalexander.jnacl.crypto.curve25519xsalsa20poly1305 ------------------------------- */
 
@@ -92,13 +118,11 @@ JNIEXPORT jint JNICALL Java_com_neilalexander_jnacl_crypto_curve25519xsalsa20pol
     (void)cls;
     if (mlen < 32)
         return -1;
-    crit_arg v[4] = {{c, mlen, 1, NULL}, {m, mlen, 0, NULL}, {n, 24, 0, NULL}, {k, 32, 0, NULL}};
-    warm_thread();
-    if (crit_acquire(env, v, 4))
+    jarr_arg v[4] = {{c, mlen, 1, NULL}, {m, mlen, 0, NULL}, {n, 24, 0, NULL}, {k, 32, 0, NULL}};
+    size_t used;
+    if (stage_in(env, v, 4, &used))
         return -1;
-    const int rc = cz_box_afternm(U8(0), U8(1), (uint64_t)mlen, U8(2), U8(3));
-    crit_release(env, v, 4);
-    return rc;
+    return stage_out(env, v, 4, used, cz_box_afternm(U8(0), U8(1), (uint64_t)mlen, U8(2), U8(3)));
 }
 
 /* Curve.java:139-147 -> crypto_box_open_afternm(m, c, clen, n, k): -1 on a bad tag */
@@ -108,13 +132,11 @@ JNIEXPORT jint JNICALL Java_com_neilalexander_jnacl_crypto_curve25519xsalsa20pol
     (void)cls;
     if (clen < 32)
         return -1;
-    crit_arg v[4] = {{m, clen, 1, NULL}, {c, clen, 0, NULL}, {n, 24, 0, NULL}, {k, 32, 0, NULL}};
-    warm_thread();
-    if (crit_acquire(env, v, 4))
+    jarr_arg v[4] = {{m, clen, 1, NULL}, {c, clen, 0, NULL}, {n, 24, 0, NULL}, {k, 32, 0, NULL}};
+    size_t used;
+    if (stage_in(env, v, 4, &used))
         return -1;
-    const int rc = cz_box_open_afternm(U8(0), U8(1), (uint64_t)clen, U8(2), U8(3));
-    crit_release(env, v, 4);
-    return rc;
+    return stage_out(env, v, 4, used, cz_box_open_afternm(U8(0), U8(1), (uint64_t)clen, U8(2), U8(3)));
 }
 
 /* Curve.java:124-127 */
@@ -122,13 +144,11 @@ JNIEXPORT jint JNICALL Java_com_neilalexander_jnacl_crypto_curve25519xsalsa20pol
     JNIEnv *env, jclass cls, jbyteArray k, jbyteArray pk, jbyteArray sk)
 {
     (void)cls;
-    crit_arg v[3] = {{k, 32, 1, NULL}, {pk, 32, 0, NULL}, {sk, 32, 0, NULL}};
-    warm_thread();
-    if (crit_acquire(env, v, 3))
+    jarr_arg v[3] = {{k, 32, 1, NULL}, {pk, 32, 0, NULL}, {sk, 32, 0, NULL}};
+    size_t used;
+    if (stage_in(env, v, 3, &used))
         return -1;
-    const int rc = cz_box_beforenm(U8(0), U8(1), U8(2));
-    crit_release(env, v, 3);
-    return rc;
+    return stage_out(env, v, 3, used, cz_box_beforenm(U8(0), U8(1), U8(2)));
 }
 
 /* Curve.java:183-193 */
@@ -138,13 +158,11 @@ JNIEXPORT jint JNICALL Java_com_neilalexander_jnacl_crypto_curve25519xsalsa20pol
     (void)cls;
     if (mlen < 32)
         return -1;
-    crit_arg v[5] = {{c, mlen, 1, NULL}, {m, mlen, 0, NULL}, {n, 24, 0, NULL}, {pk, 32, 0, NULL}, {sk, 32, 0, NULL}};
-    warm_thread();
-    if (crit_acquire(env, v, 5))
+    jarr_arg v[5] = {{c, mlen, 1, NULL}, {m, mlen, 0, NULL}, {n, 24, 0, NULL}, {pk, 32, 0, NULL}, {sk, 32, 0, NULL}};
+    size_t used;
+    if (stage_in(env, v, 5, &used))
         return -1;
-    const int rc = cz_box(U8(0), U8(1), (uint64_t)mlen, U8(2), U8(3), U8(4));
-    crit_release(env, v, 5);
-    return rc;
+    return stage_out(env, v, 5, used, cz_box(U8(0), U8(1), (uint64_t)mlen, U8(2), U8(3), U8(4)));
 }
 
 /* Curve.java:149-157 */
@@ -154,13 +172,11 @@ JNIEXPORT jint JNICALL Java_com_neilalexander_jnacl_crypto_curve25519xsalsa20pol
     (void)cls;
     if (clen < 32)
         return -1;
-    crit_arg v[5] = {{m, clen, 1, NULL}, {c, clen, 0, NULL}, {n, 24, 0, NULL}, {pk, 32, 0, NULL}, {sk, 32, 0, NULL}};
-    warm_thread();
-    if (crit_acquire(env, v, 5))
+    jarr_arg v[5] = {{m, clen, 1, NULL}, {c, clen, 0, NULL}, {n, 24, 0, NULL}, {pk, 32, 0, NULL}, {sk, 32, 0, NULL}};
+    size_t used;
+    if (stage_in(env, v, 5, &used))
         return -1;
-    const int rc = cz_box_open(U8(0), U8(1), (uint64_t)clen, U8(2), U8(3), U8(4));
-    crit_release(env, v, 5);
-    return rc;
+    return stage_out(env, v, 5, used, cz_box_open(U8(0), U8(1), (uint64_t)clen, U8(2), U8(3), U8(4)));
 }
 
 /* Curve.java:84-115 */
@@ -168,13 +184,11 @@ JNIEXPORT jint JNICALL Java_com_neilalexander_jnacl_crypto_curve25519xsalsa20pol
     JNIEnv *env, jclass cls, jbyteArray pk, jbyteArray sk)
 {
     (void)cls;
-    crit_arg v[2] = {{pk, 32, 1, NULL}, {sk, 32, 1, NULL}};
-    warm_thread();
-    if (crit_acquire(env, v, 2))
+    jarr_arg v[2] = {{pk, 32, 1, NULL}, {sk, 32, 1, NULL}};
+    size_t used;
+    if (stage_in(env, v, 2, &used))
         return -1;
-    const int rc = cz_box_keypair(U8(0), U8(1));
-    crit_release(env, v, 2);
-    return rc;
+    return stage_out(env, v, 2, used, cz_box_keypair(U8(0), U8(1)));
 }
 
 /* ---- com.neilalexander.jnacl.crypto.xsalsa20poly1305 (Curve.java:159-181: cookie boxes) ------ */
@@ -185,13 +199,11 @@ JNIEXPORT jint JNICALL Java_com_neilalexander_jnacl_crypto_xsalsa20poly1305_cryp
     (void)cls;
     if (mlen < 32)
         return -1;
-    crit_arg v[4] = {{c, mlen, 1, NULL}, {m, mlen, 0, NULL}, {n, 24, 0, NULL}, {k, 32, 0, NULL}};
-    warm_thread();
-    if (crit_acquire(env, v, 4))
+    jarr_arg v[4] = {{c, mlen, 1, NULL}, {m, mlen, 0, NULL}, {n, 24, 0, NULL}, {k, 32, 0, NULL}};
+    size_t used;
+    if (stage_in(env, v, 4, &used))
         return -1;
-    const int rc = cz_secretbox(U8(0), U8(1), (uint64_t)mlen, U8(2), U8(3));
-    crit_release(env, v, 4);
-    return rc;
+    return stage_out(env, v, 4, used, cz_secretbox(U8(0), U8(1), (uint64_t)mlen, U8(2), U8(3)));
 }
 
 JNIEXPORT jint JNICALL Java_com_neilalexander_jnacl_crypto_xsalsa20poly1305_crypto_1secretbox_1open(
@@ -200,13 +212,11 @@ JNIEXPORT jint JNICALL Java_com_neilalexander_jnacl_crypto_xsalsa20poly1305_cryp
     (void)cls;
     if (clen < 32)
         return -1;
-    crit_arg v[4] = {{m, clen, 1, NULL}, {c, clen, 0, NULL}, {n, 24, 0, NULL}, {k, 32, 0, NULL}};
-    warm_thread();
-    if (crit_acquire(env, v, 4))
+    jarr_arg v[4] = {{m, clen, 1, NULL}, {c, clen, 0, NULL}, {n, 24, 0, NULL}, {k, 32, 0, NULL}};
+    size_t used;
+    if (stage_in(env, v, 4, &used))
         return -1;
-    const int rc = cz_secretbox_open(U8(0), U8(1), (uint64_t)clen, U8(2), U8(3));
-    crit_release(env, v, 4);
-    return rc;
+    return stage_out(env, v, 4, used, cz_secretbox_open(U8(0), U8(1), (uint64_t)clen, U8(2), U8(3)));
 }
 
 /* ---- direct ByteBuffers ----------------------------------------------------------------------- */
@@ -388,12 +398,19 @@ JNIEXPORT jint JNICALL Java_zmq_io_GpuCurveEngine_addConn(JNIEnv *env, jclass cl
     (void)cls;
     if (!e)
         return CZ_EINVAL;
-    crit_arg v[1] = {{precom, 32, 0, NULL}};
-    if (crit_acquire(env, v, 1))
+    jarr_arg v[1] = {{precom, 32, 0, NULL}};
+    size_t used;
+    if (stage_in(env, v, 1, &used))
         return CZ_EINVAL;
     const int rc = cz_engine_add_conn(ENG(e), server ? 1 : 0, U8(0), (uint64_t)cnNonce, (uint64_t)cnPeerNonce);
-    crit_release(env, v, 1);
+    stage_out(env, v, 1, used, 0);  /* wipes the staged key (nothing to copy back) */
     return rc;
+}
+
+JNIEXPORT jint JNICALL Java_zmq_io_GpuCurveEngine_removeConn(JNIEnv *env, jclass cls, jlong e, jint conn)
+{
+    (void)env, (void)cls;
+    return e ? cz_engine_remove_conn(ENG(e), conn) : CZ_EINVAL;
 }
 
 JNIEXPORT jobject JNICALL Java_zmq_io_GpuCurveEngine_msgAlloc(JNIEnv *env, jclass cls, jlong e, jint len)

@@ -8,6 +8,7 @@
 #include <stdlib.h>
 #include <string.h>
 
+#include "curvezmq_mi355x.h"
 #include "jni_min.h"
 
 enum { K_BYTES = 1, K_INTS, K_DIRECT, K_CLASS, K_OBJARRAY };
@@ -18,6 +19,7 @@ struct _jobject {
     void *data;     /* array storage (owned by the test) or direct buffer address (NULL: not direct) */
     jlong cap;      /* direct buffer capacity */
     int pins, releases, last_mode;
+    int gets, sets; /* Get/SetByteArrayRegion calls */
     void *copy;     /* the live copy handed out in copy mode */
     jobject *elems; /* K_OBJARRAY */
 };
@@ -28,13 +30,16 @@ static int g_copy_mode, g_fail_pin_at = -1, g_pin_count, g_outstanding, g_calls_
  * NewDirectByteBuffer returns NULL with an OutOfMemoryError pending, as a JVM does */
 static int g_live_refs, g_max_live_refs, g_fail_new_at = -1, g_new_count, g_exception;
 static int g_modes[64], g_nmodes;
+/* library calls the shim made (through the --wrap'ed cz_* entry points below) and how many of them
+ * ran while a Java array was pinned: the GC would have been locked out across a GPU launch */
+static int g_lib_calls, g_lib_calls_pinned;
 
 static size_t elem_size(jobject o) { return o->kind == K_INTS ? 4 : 1; }
 
 static jclass f_FindClass(JNIEnv *env, const char *name)
 {
     (void)env;
-    static struct _jobject cls = {K_CLASS, 0, NULL, 0, 0, 0, 0, NULL, NULL};
+    static struct _jobject cls = {.kind = K_CLASS};
     if (g_outstanding)
         g_calls_in_critical++;
     if (strcmp(name, "java/nio/ByteBuffer") != 0) {
@@ -93,6 +98,32 @@ static void f_SetIntArrayRegion(JNIEnv *env, jintArray a, jsize start, jsize len
     (void)env;
     if (start >= 0 && start + len <= a->len)
         memcpy((jint *)a->data + start, buf, (size_t)len * 4);
+}
+
+static void f_GetByteArrayRegion(JNIEnv *env, jbyteArray a, jsize start, jsize len, jbyte *buf)
+{
+    (void)env;
+    if (g_outstanding)
+        g_calls_in_critical++;
+    a->gets++;
+    if (start < 0 || len < 0 || start + len > a->len) {
+        g_exception = 1; /* ArrayIndexOutOfBoundsException */
+        return;
+    }
+    memcpy(buf, (jbyte *)a->data + start, (size_t)len);
+}
+
+static void f_SetByteArrayRegion(JNIEnv *env, jbyteArray a, jsize start, jsize len, const jbyte *buf)
+{
+    (void)env;
+    if (g_outstanding)
+        g_calls_in_critical++;
+    a->sets++;
+    if (start < 0 || len < 0 || start + len > a->len) {
+        g_exception = 1;
+        return;
+    }
+    memcpy((jbyte *)a->data + start, buf, (size_t)len);
 }
 
 static void *f_GetPrimitiveArrayCritical(JNIEnv *env, jarray a, jboolean *isCopy)
@@ -170,6 +201,8 @@ JNIEnv *fake_env(void)
     g_table.NewObjectArray = f_NewObjectArray;
     g_table.SetObjectArrayElement = f_SetObjectArrayElement;
     g_table.SetIntArrayRegion = f_SetIntArrayRegion;
+    g_table.GetByteArrayRegion = f_GetByteArrayRegion;
+    g_table.SetByteArrayRegion = f_SetByteArrayRegion;
     g_table.GetPrimitiveArrayCritical = f_GetPrimitiveArrayCritical;
     g_table.ReleasePrimitiveArrayCritical = f_ReleasePrimitiveArrayCritical;
     g_table.NewDirectByteBuffer = f_NewDirectByteBuffer;
@@ -206,6 +239,15 @@ int fake_calls_in_critical(void) { return g_calls_in_critical; }
 int fake_nmodes(void) { return g_nmodes; }
 int fake_mode(int i) { return i >= 0 && i < g_nmodes ? g_modes[i] : -1; }
 int fake_pins(jobject o) { return o->pins; }
+int fake_gets(jobject o) { return o->gets; }
+int fake_sets(jobject o) { return o->sets; }
+int fake_lib_calls(void) { return g_lib_calls; }
+int fake_lib_calls_pinned(void) { return g_lib_calls_pinned; }
+void fake_reset_lib_calls(void) { g_lib_calls = g_lib_calls_pinned = 0; }
+void fake_raise(void) { g_exception = 1; }
+/* hold an array pinned from the test (as another native of the thread might), and let it go */
+void fake_pin(jobject o) { o->pins++, g_outstanding++; }
+void fake_unpin(jobject o) { o->releases++, g_outstanding--; }
 int fake_releases(jobject o) { return o->releases; }
 int fake_last_mode(jobject o) { return o->last_mode; }
 int fake_kind(jobject o) { return o ? o->kind : 0; }
@@ -213,3 +255,61 @@ jsize fake_len(jobject o) { return o->len; }
 jobject fake_elem(jobject o, jsize i) { return o->elems[i]; }
 void *fake_addr(jobject o) { return o->data; }
 jlong fake_cap(jobject o) { return o->cap; }
+
+/* The library entry points the byte[] natives call, interposed with -Wl,--wrap=<name> in the test
+ * build: each call is counted, and counted again if any Java array is pinned at that moment. */
+#define CZ_WRAP_NOTE() (g_lib_calls++, g_lib_calls_pinned += g_outstanding != 0)
+int __real_cz_box_afternm(uint8_t *, const uint8_t *, uint64_t, const uint8_t *, const uint8_t *);
+int __real_cz_box_open_afternm(uint8_t *, const uint8_t *, uint64_t, const uint8_t *, const uint8_t *);
+int __real_cz_secretbox(uint8_t *, const uint8_t *, uint64_t, const uint8_t *, const uint8_t *);
+int __real_cz_secretbox_open(uint8_t *, const uint8_t *, uint64_t, const uint8_t *, const uint8_t *);
+int __real_cz_box_beforenm(uint8_t *, const uint8_t *, const uint8_t *);
+int __real_cz_box(uint8_t *, const uint8_t *, uint64_t, const uint8_t *, const uint8_t *, const uint8_t *);
+int __real_cz_box_open(uint8_t *, const uint8_t *, uint64_t, const uint8_t *, const uint8_t *, const uint8_t *);
+int __real_cz_box_keypair(uint8_t *, uint8_t *);
+int __real_cz_engine_add_conn(cz_engine *, int, const uint8_t *, uint64_t, uint64_t);
+int __wrap_cz_box_afternm(uint8_t *c, const uint8_t *m, uint64_t l, const uint8_t *n, const uint8_t *k)
+{
+    CZ_WRAP_NOTE();
+    return __real_cz_box_afternm(c, m, l, n, k);
+}
+int __wrap_cz_box_open_afternm(uint8_t *m, const uint8_t *c, uint64_t l, const uint8_t *n, const uint8_t *k)
+{
+    CZ_WRAP_NOTE();
+    return __real_cz_box_open_afternm(m, c, l, n, k);
+}
+int __wrap_cz_secretbox(uint8_t *c, const uint8_t *m, uint64_t l, const uint8_t *n, const uint8_t *k)
+{
+    CZ_WRAP_NOTE();
+    return __real_cz_secretbox(c, m, l, n, k);
+}
+int __wrap_cz_secretbox_open(uint8_t *m, const uint8_t *c, uint64_t l, const uint8_t *n, const uint8_t *k)
+{
+    CZ_WRAP_NOTE();
+    return __real_cz_secretbox_open(m, c, l, n, k);
+}
+int __wrap_cz_box_beforenm(uint8_t *k, const uint8_t *pk, const uint8_t *sk)
+{
+    CZ_WRAP_NOTE();
+    return __real_cz_box_beforenm(k, pk, sk);
+}
+int __wrap_cz_box(uint8_t *c, const uint8_t *m, uint64_t l, const uint8_t *n, const uint8_t *pk, const uint8_t *sk)
+{
+    CZ_WRAP_NOTE();
+    return __real_cz_box(c, m, l, n, pk, sk);
+}
+int __wrap_cz_box_open(uint8_t *m, const uint8_t *c, uint64_t l, const uint8_t *n, const uint8_t *pk, const uint8_t *sk)
+{
+    CZ_WRAP_NOTE();
+    return __real_cz_box_open(m, c, l, n, pk, sk);
+}
+int __wrap_cz_box_keypair(uint8_t *pk, uint8_t *sk)
+{
+    CZ_WRAP_NOTE();
+    return __real_cz_box_keypair(pk, sk);
+}
+int __wrap_cz_engine_add_conn(cz_engine *e, int server, const uint8_t *precom, uint64_t a, uint64_t b)
+{
+    CZ_WRAP_NOTE();
+    return __real_cz_engine_add_conn(e, server, precom, a, b);
+}

@@ -21,6 +21,9 @@ public final class GpuCurveEngine
 
     public static native int addConn(long e, boolean server, byte[] precom, long cnNonce, long cnPeerNonce);
 
+    // the connection is gone (StreamEngine unplug / error): its id is reused by a later addConn
+    public static native int removeConn(long e, int conn);
+
     public static native ByteBuffer msgAlloc(long e, int len);
 
     public static native int send(long e, int conn, ByteBuffer payload, int len, int flags);

@@ -8,23 +8,27 @@
 //   inEvent   (StreamEngine.java:379-465): SocketChannel.read, V2Decoder, decodeAndPush =
 //             mechanism.decode + session.pushMsg (:1067-1098), error(PROTOCOL) on a failed decode.
 // Here outEvent(conn) only pulls and queues (GpuCurveEngine.send), inEvent(conn) only reads and
-// queues (GpuCurveEngine.recv); the poller calls endOfLoop() once per iteration, which seals every
-// queued message of every connection (flushOut), writes each connection's wire bytes with one
-// gathering write (wireIov), opens every received frame (flushIn) and delivers the payloads in
-// order.  A connection whose frame fails (bad tag, replay, malformed, framing) gets the reference's
+// queues (GpuCurveEngine.recv); the poller calls endOfLoop() once per iteration, which opens every
+// received frame (flushIn) and delivers the payloads in order, then seals every queued message of
+// every connection (flushOut) and writes each connection's wire bytes with one gathering write
+// (wireIov).  A connection whose frame fails (bad tag, replay, malformed, framing) gets the reference's
 // monitor event (connError -> eventHandshakeFailedProtocol) and is torn down, as decodeAndPush
 // returning false tears it down; the other connections carry on.
 //
-// StreamEngine keeps the rest of its role (handshake, heartbeats, metadata): it hands a connection
-// to attach() once mechanism.status() == READY and implements Sink with its own pullMsg / decodeAndPush
-// tail.  One hook per IO thread (the engine is not thread-safe).
+// The wiring into the reference is jni/patches/jeromq-gpu-curve.patch (INTEGRATION.md section 5):
+// Poller owns one hook per IO thread (fromSystemProperties, -Dzmq.curve.gpu=true) and calls
+// endOfLoop() at the end of every loop iteration; StreamEngine attaches a CURVE connection when
+// its mechanism reaches READY, hands over the bytes its decoder had already read, delegates
+// outEvent / inEvent, and detaches on teardown.  StreamEngine keeps the rest of its role
+// (handshake, heartbeats, metadata, back-pressure) through Sink.  Not thread-safe: one per IO thread.
 package zmq.io;
 
 import java.io.IOException;
+import java.lang.reflect.Field;
 import java.nio.ByteBuffer;
 import java.nio.channels.GatheringByteChannel;
 import java.nio.channels.ReadableByteChannel;
-import java.lang.reflect.Field;
+import java.util.ArrayDeque;
 import java.util.ArrayList;
 import java.util.List;
 
@@ -32,8 +36,6 @@ import zmq.Msg;
 import zmq.io.mechanism.Mechanism;
 import zmq.io.mechanism.curve.CurveClientMechanism;
 import zmq.io.mechanism.curve.CurveServerMechanism;
-import zmq.io.mechanism.curve.PinnedMsgAllocator;
-import zmq.msg.MsgAllocator;
 
 public final class GpuCurveIoHook implements AutoCloseable
 {
@@ -41,20 +43,38 @@ public final class GpuCurveIoHook implements AutoCloseable
     private static final int CZ_OK     = 0;
     private static final int CZ_ENOMEM = -12;
 
+    // -Dzmq.curve.gpu=true turns the hook on for every IO thread; the sizes and the device are
+    // -Dzmq.curve.gpu.arena (pinned outbound payload bytes per loop), -Dzmq.curve.gpu.read (receive
+    // buffer) and -Dzmq.curve.gpu.device
+    public static final String PROPERTY = "zmq.curve.gpu";
+
     // The StreamEngine side of one connection.
     public interface Sink
     {
         // the next message to send, or null (StreamEngine.pullAndEncode without the encode:
-        // session.pullMsg, :1052-1063)
+        // session.pullMsg, :1052-1063; a heartbeat PING / PONG command when one is due)
         Msg pull();
 
         // a decoded message (StreamEngine.decodeAndPush after mechanism.decode, :1072-1097: commands
-        // to processCommand, metadata, session.pushMsg); false stops delivery on this connection
+        // to processCommand, metadata, session.pushMsg); false: the session refused it (back-pressure,
+        // the engine stops reading until restartInput) -- the hook keeps it and the rest for resume()
         boolean push(Msg msg);
 
         // the connection failed: the reference's monitor event (0 for a V2 framing error, which
         // raises none), then error(ErrorReason.PROTOCOL) (StreamEngine.java:452-456)
         void failed(int event);
+
+        // the hook needs another outEvent for this connection (socket backlog, or a message held
+        // back by a full arena): StreamEngine sets POLLOUT (ioObject.setPollOut)
+        void wantOutput();
+
+        // the end of one loop's deliveries to this connection: StreamEngine flushes the session
+        // (inEvent's session.flush(), StreamEngine.java:463-464)
+        void delivered();
+
+        // false while StreamEngine still has bytes of its own to write (the last handshake command,
+        // outsize > 0): the sealed frames wait behind them
+        boolean writable();
     }
 
     private static final class Conn
@@ -66,7 +86,9 @@ public final class GpuCurveIoHook implements AutoCloseable
         boolean                    queued;      // has messages in the current flushOut
         boolean                    received;    // has bytes for the current flushIn
         ByteBuffer                 backlog;     // wire bytes a non-blocking write left over
+        ArrayDeque<Msg>            undelivered; // decoded messages the session has not taken yet
         boolean                    failed;
+        boolean                    outputDead;  // a socket write failed: no more output (StreamEngine.java:518-524)
 
         Conn(int id, Sink sink, GatheringByteChannel out)
         {
@@ -76,11 +98,10 @@ public final class GpuCurveIoHook implements AutoCloseable
         }
     }
 
-    private final long               engine;
-    private final PinnedMsgAllocator allocator;
-    private final List<Conn>         conns   = new ArrayList<>();
-    private final ByteBuffer         readBuf;
-    private final int[]              scratch = new int[1];
+    private final long       engine;
+    private final List<Conn> conns   = new ArrayList<>();
+    private final ByteBuffer readBuf;
+    private final int[]      scratch = new int[1];
 
     // arenaBytes: pinned outbound payload arena (messages per loop); readBytes: receive buffer
     public GpuCurveIoHook(long arenaBytes, int readBytes, int device)
@@ -89,19 +110,36 @@ public final class GpuCurveIoHook implements AutoCloseable
         if (engine == 0) {
             throw new IllegalStateException("GpuCurveEngine.create failed (no MI355X visible?)");
         }
-        allocator = PinnedMsgAllocator.overEngine(engine);
         readBuf = ByteBuffer.allocateDirect(readBytes);
     }
 
-    // ZMQ_MSG_ALLOCATOR for the sockets this IO thread serves: payloads written into these Msgs are
-    // sealed straight from the pinned arena
-    public MsgAllocator allocator()
+    // the hook Poller creates for its IO thread, or null when -Dzmq.curve.gpu is not true
+    public static GpuCurveIoHook fromSystemProperties()
     {
-        return allocator;
+        if (!Boolean.getBoolean(PROPERTY)) {
+            return null;
+        }
+        return new GpuCurveIoHook(Long.getLong(PROPERTY + ".arena", 256L << 20),
+                                  Integer.getInteger(PROPERTY + ".read", 1 << 20),
+                                  Integer.getInteger(PROPERTY + ".device", 0));
+    }
+
+    // A pinned payload for an application send on an attached connection: the application writes
+    // its bytes into the Msg and sends it; the engine seals it in place (no staging copy).  The bytes
+    // belong to the engine's outbound arena, which is reused after the flush that sends the Msg, so
+    // the Msg must be sent, once, before the next endOfLoop and not touched after.  Null when the
+    // arena is full (send a heap Msg instead: it is copied once).  This is NOT a ZMQ_MSG_ALLOCATOR:
+    // the reference hands that option to its decoders, i.e. to INBOUND frames
+    // (StreamEngine.java:735-805, Decoder.java:102), whose lifetime the application controls.
+    public Msg pinnedMsg(int size)
+    {
+        ByteBuffer b = GpuCurveEngine.msgAlloc(engine, size);
+        return b != null ? new Msg(b) : null;
     }
 
     // A CURVE connection whose handshake is complete (mechanism.status() == READY): its cnPrecom and
-    // nonce counters move into the engine, which seals and opens every MESSAGE from now on.
+    // nonce counters move into the engine, which seals and opens every MESSAGE from now on.  The
+    // mechanism must not encode or decode another message after this call.
     public int attach(Mechanism mechanism, Sink sink, GatheringByteChannel out)
     {
         final boolean server;
@@ -128,6 +166,18 @@ public final class GpuCurveIoHook implements AutoCloseable
         return id;
     }
 
+    // The connection is gone (StreamEngine unplug / error): its queued and received data are
+    // dropped and its engine id is reused by a later attach.
+    public void detach(int conn)
+    {
+        Conn c = conns.get(conn);
+        if (c == null) {
+            return;
+        }
+        conns.set(conn, null);
+        GpuCurveEngine.removeConn(engine, conn);
+    }
+
     // CurveClientMechanism / CurveServerMechanism keep the session keys private
     // (CurveClientMechanism.java:46-49, CurveServerMechanism.java:34-47)
     private static Object field(Mechanism m, String name)
@@ -143,22 +193,24 @@ public final class GpuCurveIoHook implements AutoCloseable
     }
 
     // StreamEngine.outEvent for an attached connection: pull every message the session has and
-    // queue it for this loop's flush.  Nothing is sealed or written here.
-    public void outEvent(int conn)
+    // queue it for this loop's flush.  Nothing is sealed or written here.  True when something is
+    // queued or held for a later loop.
+    public boolean outEvent(int conn)
     {
         Conn c = conns.get(conn);
-        if (c.failed) {
-            return;
+        if (c == null || c.failed || c.outputDead) {
+            return false;
         }
         Msg msg = c.held != null ? c.held : c.sink.pull();
         c.held = null;
         while (msg != null) {
             if (!queue(c, msg)) {
                 c.held = msg;      // the arena is full: this one leads the next loop
-                return;
+                return true;
             }
             msg = c.sink.pull();
         }
+        return c.queued;
     }
 
     private boolean queue(Conn c, Msg msg)
@@ -167,7 +219,7 @@ public final class GpuCurveIoHook implements AutoCloseable
         final int flags = (msg.hasMore() ? Msg.MORE : 0) | (msg.isCommand() ? Msg.COMMAND : 0);
         ByteBuffer payload = msg.buf();   // position 0: Msg never moves its buffer's position
         if (!payload.isDirect()) {
-            // a heap payload (not from allocator()): one copy into the arena
+            // a heap payload (not from pinnedMsg()): one copy into the arena
             ByteBuffer pinned = GpuCurveEngine.msgAlloc(engine, size);
             if (pinned == null) {
                 return false;
@@ -204,52 +256,101 @@ public final class GpuCurveIoHook implements AutoCloseable
             if (n == 0) {
                 return total;
             }
-            if (!c.failed && GpuCurveEngine.recv(engine, c.id, readBuf, n) != CZ_OK) {
-                fail(c);
+            total += n;
+            if (c == null || c.failed) {
+                continue;          // drain the socket; the bytes of a failed connection go nowhere
+            }
+            if (GpuCurveEngine.recv(engine, c.id, readBuf, n) != CZ_OK) {
+                fail(c);           // tears the connection down (StreamEngine.error): stop reading
+                return total;
             }
             c.received = true;
-            total += n;
         }
     }
 
-    // Once per poller loop: seal and write every connection's queued messages, open and deliver
-    // every connection's received frames.  Returns the connections whose output is not fully written
-    // (the caller keeps POLLOUT on them and calls writeBacklog from their next outEvent).
-    public List<Integer> endOfLoop() throws IOException
+    // Wire bytes StreamEngine's decoder had read past the frame that completed the handshake (the
+    // peer's first MESSAGEs can share a TCP read with its READY): they start at a frame boundary and
+    // go to the engine ahead of anything read later.
+    public void handOver(int conn, ByteBuffer data, int len)
     {
-        List<Integer> blocked = new ArrayList<>();
-        boolean anyOut = false;
-        boolean anyIn = false;
-        for (Conn c : conns) {
-            if (c != null) {
-                anyOut |= c.queued;
-                anyIn |= c.received;
+        Conn c = conns.get(conn);
+        if (c == null || c.failed || len <= 0) {
+            return;
+        }
+        ByteBuffer src = data.duplicate();
+        src.limit(src.position() + len);
+        while (src.hasRemaining()) {
+            readBuf.clear();
+            int n = Math.min(readBuf.capacity(), src.remaining());
+            ByteBuffer part = src.duplicate();
+            part.limit(part.position() + n);
+            readBuf.put(part);
+            src.position(src.position() + n);
+            if (GpuCurveEngine.recv(engine, c.id, readBuf, n) != CZ_OK) {
+                fail(c);
+                return;
             }
         }
-        if (anyOut) {
-            if (GpuCurveEngine.flushOut(engine) != CZ_OK) {
-                throw new IOException("GpuCurveEngine.flushOut failed");
-            }
-            for (Conn c : conns) {
-                if (c == null || !c.queued) {
-                    continue;
-                }
-                c.queued = false;
-                if (!write(c)) {
-                    blocked.add(c.id);
-                }
-            }
+        c.received = true;
+    }
+
+    // Once per poller loop: open and deliver every connection's received frames, then seal and
+    // write every connection's queued messages -- in that order, so a reply queued during delivery
+    // (a heartbeat PONG, StreamEngine.java:1217-1246) leaves in the same loop.  Returns the
+    // connections whose output is not fully written or that hold a message back; each of those has
+    // been asked for another outEvent (Sink.wantOutput).
+    public List<Integer> endOfLoop() throws IOException
+    {
+        boolean anyIn = false;
+        for (Conn c : conns) {
+            anyIn |= c != null && c.received;
         }
         if (anyIn) {
             if (GpuCurveEngine.flushIn(engine) != CZ_OK) {
                 throw new IOException("GpuCurveEngine.flushIn failed");
             }
-            for (Conn c : conns) {
+            for (int i = 0; i < conns.size(); i++) {
+                Conn c = conns.get(i);
                 if (c == null || !c.received) {
                     continue;
                 }
                 c.received = false;
                 deliver(c);
+                if (conns.get(i) == c) {
+                    c.sink.delivered();
+                }
+            }
+        }
+        List<Integer> blocked = new ArrayList<>();
+        boolean anyOut = false;
+        for (Conn c : conns) {
+            anyOut |= c != null && c.queued;
+        }
+        if (!anyOut) {
+            return blocked;
+        }
+        if (GpuCurveEngine.flushOut(engine) != CZ_OK) {
+            throw new IOException("GpuCurveEngine.flushOut failed");
+        }
+        for (Conn c : conns) {
+            if (c == null || !c.queued) {
+                continue;
+            }
+            c.queued = false;
+            boolean done;
+            try {
+                done = write(c);
+            }
+            catch (IOException e) {
+                // as StreamEngine.outEvent on a write error: stop output, keep reading, so the input
+                // side sees the disconnect and no incoming message is lost (:518-524)
+                c.outputDead = true;
+                c.backlog = null;
+                continue;
+            }
+            if (!done || c.held != null) {
+                blocked.add(c.id);
+                c.sink.wantOutput();
             }
         }
         return blocked;
@@ -260,14 +361,18 @@ public final class GpuCurveIoHook implements AutoCloseable
     // because the next flushOut reuses the output
     private boolean write(Conn c) throws IOException
     {
-        if (!writeBacklog(c)) {
-            // earlier bytes are still waiting: these go behind them
-            appendBacklog(c, GpuCurveEngine.wireIov(engine, c.id));
-            return false;
-        }
         ByteBuffer[] pieces = GpuCurveEngine.wireIov(engine, c.id);
         if (pieces == null) {
             throw new IOException("GpuCurveEngine.wireIov failed");
+        }
+        if (!c.sink.writable()) {
+            appendBacklog(c, pieces);   // the engine's own bytes leave first
+            return false;
+        }
+        if (!writeBacklog(c)) {
+            // earlier bytes are still waiting: these go behind them
+            appendBacklog(c, pieces);
+            return false;
         }
         long left = 0;
         for (ByteBuffer p : pieces) {
@@ -287,7 +392,8 @@ public final class GpuCurveIoHook implements AutoCloseable
     // write bytes left over by an earlier loop; true when none are left
     public boolean writeBacklog(int conn) throws IOException
     {
-        return writeBacklog(conns.get(conn));
+        Conn c = conns.get(conn);
+        return c == null || c.outputDead || writeBacklog(c);
     }
 
     private boolean writeBacklog(Conn c) throws IOException
@@ -323,14 +429,15 @@ public final class GpuCurveIoHook implements AutoCloseable
     }
 
     // the frames of the last flushIn in order, then the connection's failure if it has one: every
-    // frame before the failing one is delivered, none after it (decodeAndPush returning false)
+    // frame before the failing one is delivered, none after it (decodeAndPush returning false).  The
+    // payloads are pinned engine memory valid until the next flushIn, so each becomes a heap Msg
+    // (the reference's decoder also allocates per message); what the session refuses waits in
+    // `undelivered` for resume().
     private void deliver(Conn c)
     {
         int n = GpuCurveEngine.msgsIn(engine, c.id);
         for (int i = 0; i < n; i++) {
             ByteBuffer p = GpuCurveEngine.msgIn(engine, c.id, i, scratch);
-            // the payload is pinned engine memory, valid until the next flushIn: the pipe may hold
-            // the Msg longer, so it takes a copy (the reference's decoder also allocates per message)
             byte[] data = new byte[p.remaining()];
             p.get(data);
             Msg msg = new Msg(data);
@@ -340,14 +447,42 @@ public final class GpuCurveIoHook implements AutoCloseable
             if ((scratch[0] & Msg.COMMAND) != 0) {
                 msg.setFlags(Msg.COMMAND);
             }
-            if (!c.sink.push(msg)) {
-                break;
+            if (c.undelivered != null) {
+                c.undelivered.add(msg);
             }
+            else if (!c.sink.push(msg)) {
+                if (conns.get(c.id) != c) {
+                    return;        // the push tore the connection down (StreamEngine.error -> detach)
+                }
+                c.undelivered = new ArrayDeque<>();
+                c.undelivered.add(msg);
+            }
+        }
+        if (conns.get(c.id) != c) {
+            return;
         }
         if (!c.failed && GpuCurveEngine.connError(engine, c.id, scratch) != CZ_OK) {
             c.failed = true;
             c.sink.failed(scratch[0]);
         }
+    }
+
+    // StreamEngine.restartInput for an attached connection: push what the session refused earlier.
+    // True when everything is delivered (the engine may read again).
+    public boolean resume(int conn)
+    {
+        Conn c = conns.get(conn);
+        if (c == null || c.undelivered == null) {
+            return true;
+        }
+        while (!c.undelivered.isEmpty()) {
+            if (!c.sink.push(c.undelivered.peekFirst())) {
+                return false;
+            }
+            c.undelivered.pollFirst();
+        }
+        c.undelivered = null;
+        return true;
     }
 
     private void fail(Conn c)
@@ -363,7 +498,6 @@ public final class GpuCurveIoHook implements AutoCloseable
     @Override
     public void close()
     {
-        allocator.close();
         GpuCurveEngine.destroy(engine);
     }
 }

@@ -113,6 +113,25 @@ final class GpuCurveMessageBatch implements AutoCloseable
         return (v + 15) & ~15L;
     }
 
+    private static final byte[] ZEROS = new byte[1 << 16];
+
+    // plaintext must not outlive the call in pinned memory (the C paths explicit_bzero their
+    // staging): zero the first n bytes of b
+    private static void wipe(ByteBuffer b, long n)
+    {
+        if (b == null) {
+            return;
+        }
+        ByteBuffer d = b.duplicate();
+        d.clear();
+        long left = Math.min(n, d.capacity());
+        while (left > 0) {
+            int k = (int) Math.min(left, ZEROS.length);
+            d.put(ZEROS, 0, k);
+            left -= k;
+        }
+    }
+
     private void desc(int i, long inOff, long outOff, int len, long counter, int flags, int prev)
     {
         int d = i * DESC_BYTES;
@@ -156,8 +175,10 @@ final class GpuCurveMessageBatch implements AutoCloseable
             oo += m.size() + OVERHEAD;
         }
         if (GpuCurveBatch.seal(sealCtx, descs, count, in, out) != CZ_OK) {
+            wipe(in, io);
             throw new IllegalStateException("GpuCurveBatch.seal failed");
         }
+        wipe(in, io);   // the staged plaintext
         cnNonce += count;
         List<Msg> encoded = new ArrayList<>(count);
         for (int i = 0; i < count; i++) {
@@ -204,6 +225,7 @@ final class GpuCurveMessageBatch implements AutoCloseable
         }
         lastEvent = 0;
         if (GpuCurveBatch.open(openCtx, descs, count, in, out, status) != CZ_OK) {
+            wipe(out, oo);
             throw new IllegalStateException("GpuCurveBatch.open failed");
         }
         List<Msg> decoded = new ArrayList<>(count);
@@ -231,6 +253,7 @@ final class GpuCurveMessageBatch implements AutoCloseable
             p.put(out, (int) descs.getLong(d + 8), size - OVERHEAD);
             decoded.add(p);
         }
+        wipe(out, oo);   // every opened plaintext, including frames after a failure
         return decoded;
     }
 
@@ -271,6 +294,7 @@ final class GpuCurveMessageBatch implements AutoCloseable
         }
         for (ByteBuffer b : new ByteBuffer[] {descs, in, out, status}) {
             if (b != null) {
+                wipe(b, b.capacity());
                 GpuCurveBatch.hostFree(b);
             }
         }

@@ -52,7 +52,11 @@ struct JNINativeInterface_ {
     jobjectArray (*NewObjectArray)(JNIEnv *env, jsize len, jclass cls, jobject init);        /* 172 */
     void *GetObjectArrayElement;                                                              /* 173 */
     void (*SetObjectArrayElement)(JNIEnv *env, jobjectArray array, jsize index, jobject val); /* 174 */
-    CZ_JNI_PAD(175, 211);
+    CZ_JNI_PAD(175, 200);
+    void (*GetByteArrayRegion)(JNIEnv *env, jbyteArray array, jsize start, jsize len, jbyte *buf);   /* 200 */
+    CZ_JNI_PAD(201, 208);
+    void (*SetByteArrayRegion)(JNIEnv *env, jbyteArray array, jsize start, jsize len, const jbyte *buf); /* 208 */
+    CZ_JNI_PAD(209, 211);
     void (*SetIntArrayRegion)(JNIEnv *env, jintArray array, jsize start, jsize len, const jint *buf); /* 211 */
     CZ_JNI_PAD(212, 222);
     void *(*GetPrimitiveArrayCritical)(JNIEnv *env, jarray array, jboolean *isCopy);          /* 222 */
@@ -72,6 +76,8 @@ CZ_JNI_SLOT(DeleteLocalRef, 23);
 CZ_JNI_SLOT(GetArrayLength, 171);
 CZ_JNI_SLOT(NewObjectArray, 172);
 CZ_JNI_SLOT(SetObjectArrayElement, 174);
+CZ_JNI_SLOT(GetByteArrayRegion, 200);
+CZ_JNI_SLOT(SetByteArrayRegion, 208);
 CZ_JNI_SLOT(SetIntArrayRegion, 211);
 CZ_JNI_SLOT(GetPrimitiveArrayCritical, 222);
 CZ_JNI_SLOT(ReleasePrimitiveArrayCritical, 223);

@@ -183,13 +183,14 @@ class _FakePopen:
 
     def __init__(self, out, rc=0):
         self.out, self.rc, self.cmd = out, rc, None
+        self.pid = -1
 
     def __call__(self, cmd, **kw):
         self.cmd, self.kw = cmd, kw
         self.stdout = iter(self.out)
         return self
 
-    def wait(self):
+    def wait(self, timeout=None):
         return self.rc
 
 
@@ -227,7 +228,7 @@ def test_bench_gpus_n_launches_child_ranks_without_touching_gpu(capsys):
     ([_rank_line(1)], 0),                    # ranks timed fewer GPUs than asked
     ([_rank_line(2), _rank_line(2)], 0),     # more than one JSON line
     ([], 0),                                 # no line at all
-    ([_rank_line(2)], 3),                    # a rank failed: its exit status is passed on
+    ([], 3),                                 # a rank failed before the line: its exit status is passed on
     ([_rank_line(2, roofline=False)], 0),    # N > 1 line without the slowest-rank roofline
     ([_rank_line(2, cpu=False)], 0),         # N > 1 line without the CPU baseline
 ])
@@ -261,3 +262,141 @@ def test_bench_refuses_world_size_mismatch(monkeypatch):
     monkeypatch.delenv("CZ_DIST_BACKEND", raising=False)
     with pytest.raises(SystemExit, match="need 2 GPUs for RCCL"):   # no GPU here: nccl refused, not faked
         bench.setup_dist(argparse.Namespace(gpus=2))
+
+
+def test_bench_launcher_relays_a_good_line_despite_a_late_rank_failure(capsys):
+    """A rank that fails after rank 0's main line is out (in the optional leg) no longer costs the
+    scaling line: the line is relayed with the exit status recorded."""
+    import json
+    import bench
+    rc = bench.launch_ranks(2, ["--gpus", "2"], popen=_FakePopen([_rank_line(2)], 3))
+    assert rc == 0
+    line = json.loads([ln for ln in capsys.readouterr().out.splitlines() if ln.startswith("{")][0])
+    assert line["ranks_exit_status"] == 3
+
+
+# --- VERDICT r05 item 1: the N > 1 line survives its optional RCCL scatter/gather leg -------------
+# Stand-in children are real processes (python -c) in their own session, as torch.distributed.run
+# is: they print a rank-0 main line, then (a) hang, (b) report a failed leg, or (c) report a good one.
+
+def _main_line_pending(n):
+    import json
+    line = json.loads(_rank_line(n))
+    line["scatter_gather"] = {"pending": True}
+    return json.dumps(line)
+
+
+def _stand_in(script):
+    import sys
+    return [sys.executable, "-c", script]
+
+
+def _alive(pid):
+    try:
+        with open(f"/proc/{pid}/status") as f:
+            return not any(ln.startswith("State:") and "Z" in ln.split()[1] for ln in f)
+    except OSError:
+        return False
+
+
+def test_launcher_kills_ranks_that_hang_in_the_leg(tmp_path, capsys):
+    import json
+    import time
+    import bench
+    pidfile = tmp_path / "pids"
+    script = f"""
+import subprocess, sys, time, os
+kid = subprocess.Popen([sys.executable, "-c", "import time; time.sleep(600)"])   # a 'rank'
+open({str(pidfile)!r}, "w").write(f"{{os.getpid()}} {{kid.pid}}")
+print('rank chatter', flush=True)
+print({_main_line_pending(2)!r}, flush=True)
+time.sleep(600)
+"""
+    t0 = time.monotonic()
+    rc = bench.launch_ranks(2, ["--gpus", "2"], cmd=_stand_in(script), leg_deadline_s=2.0)
+    took = time.monotonic() - t0
+    assert rc == 0 and took < 60
+    out = capsys.readouterr()
+    lines = [ln for ln in out.out.splitlines() if ln.startswith("{")]
+    assert len(lines) == 1
+    line = json.loads(lines[0])
+    assert line["n_gpus"] == 2 and "timeout" in line["scatter_gather"]["error"]
+    assert "killing their process group" in out.err
+    parent, kid = (int(x) for x in pidfile.read_text().split())
+    deadline = time.monotonic() + 10
+    while (_alive(parent) or _alive(kid)) and time.monotonic() < deadline:
+        time.sleep(0.1)
+    assert not _alive(parent) and not _alive(kid), "stand-in ranks survived the launcher's kill"
+
+
+def test_launcher_records_a_failed_leg(capsys):
+    import json
+    import bench
+    script = f"""
+print({_main_line_pending(2)!r}, flush=True)
+print('SCATTER_GATHER {{"error": "DistBackendError: RCCL init failed"}}', flush=True)
+raise SystemExit(1)
+"""
+    rc = bench.launch_ranks(2, ["--gpus", "2"], cmd=_stand_in(script), leg_deadline_s=60.0)
+    assert rc == 0
+    line = json.loads([ln for ln in capsys.readouterr().out.splitlines() if ln.startswith("{")][0])
+    assert line["scatter_gather"] == {"error": "DistBackendError: RCCL init failed"}
+    assert line["ranks_exit_status"] == 1
+
+
+def test_launcher_merges_a_good_leg(capsys):
+    import json
+    import bench
+    script = f"""
+print({_main_line_pending(2)!r}, flush=True)
+print('leg chatter', flush=True)
+print('SCATTER_GATHER {{"backend": "nccl (RCCL)", "verified": true, "e2e_GiBps": 9.5}}', flush=True)
+"""
+    rc = bench.launch_ranks(2, ["--gpus", "2"], cmd=_stand_in(script), leg_deadline_s=60.0)
+    assert rc == 0
+    out = capsys.readouterr()
+    lines = [ln for ln in out.out.splitlines() if ln.startswith("{")]
+    assert len(lines) == 1
+    line = json.loads(lines[0])
+    assert line["scatter_gather"] == {"backend": "nccl (RCCL)", "verified": True, "e2e_GiBps": 9.5}
+    assert "ranks_exit_status" not in line and "leg chatter" in out.err
+
+
+def test_launcher_reports_a_leg_that_never_reported():
+    """ranks that exit cleanly after a pending main line without a leg line: an error, not a hang"""
+    import bench
+    import io
+    import contextlib
+    buf = io.StringIO()
+    with contextlib.redirect_stdout(buf):
+        rc = bench.launch_ranks(2, ["--gpus", "2"], cmd=_stand_in(f"print({_main_line_pending(2)!r})"))
+    import json
+    line = json.loads(buf.getvalue().splitlines()[-1])
+    assert rc == 0 and "without reporting" in line["scatter_gather"]["error"]
+
+
+@pytest.mark.parametrize("body,expect", [
+    ("import time; time.sleep(120)", "timeout"),              # a collective that never returns
+    ("1 / 0", "ZeroDivisionError"),                           # a leg that raises
+    ("{'verified': True}", None),                             # a good leg
+])
+def test_rank_side_leg_watchdog(body, expect):
+    """bench.run_leg on rank 0: the leg's result, its exception, or (watchdog) a timeout is printed on
+    the SCATTER_GATHER line and the rank exits 0 -- within seconds, whatever the leg does."""
+    import json
+    import subprocess
+    import sys
+    here = os.path.dirname(os.path.abspath(__file__))
+    code = (f"import sys; sys.path.insert(0, {os.path.dirname(here)!r}); import bench\n"
+            f"def leg():\n    return eval(compile({body!r}, 'leg', 'exec' if 'import' in {body!r} else 'eval'))\n"
+            "r = bench.run_leg(leg, 0, 2.0)\nprint('returned', flush=True)\n")
+    r = subprocess.run([sys.executable, "-c", code], capture_output=True, text=True, timeout=90)
+    assert r.returncode == 0, r.stderr[-2000:]
+    sg = [ln for ln in r.stdout.splitlines() if ln.startswith("SCATTER_GATHER ")]
+    assert len(sg) == 1, r.stdout
+    res = json.loads(sg[0][len("SCATTER_GATHER "):])
+    if expect is None:
+        assert res == {"verified": True} and "returned" in r.stdout
+    else:
+        assert expect in res["error"]
+        assert ("returned" in r.stdout) == (expect != "timeout")

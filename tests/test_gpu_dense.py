@@ -313,3 +313,47 @@ def test_open_uniform_phase_sorted_carry(torch_dev, subkeys, n, stride, base, ta
             assert st[i] & 0xff == _lib.CZ_STATUS_OK and st[i] >> 8 == fl[i], f"frame {i} status {st[i]:#x}"
             assert p.tobytes() == hin[i * in_stride:i * in_stride + n].tobytes(), f"frame {i}"
         assert not plain[i * plain_stride + n:(i + 1) * plain_stride].any(), f"slot {i} padding"
+
+
+# EmitShiftLinesT keeps flag bits 28..31 above an output's end d + total, so the
+# launchers send one frame to the byte-shifted emitter only while d + total < 2^28
+# (SHIFT_TOTAL_MAX = 2^28 - 128 in cz_kernels.hip).  One frame at the bound (shifted emitter, its
+# end field at 2^28 - 1 with d = 127) and one just above it (lane-wise stores), output 127 bytes
+# into a line, 16-byte aligned payload: the whole body against the oracle, the bytes around it kept.
+SHIFT_TOTAL_MAX = (1 << 28) - 128
+
+
+@pytest.mark.parametrize("total", [SHIFT_TOTAL_MAX, SHIFT_TOTAL_MAX + 1])
+def test_seal_uniform_single_frame_at_shift_bound(torch_dev, subkeys, total):
+    torch, dev = torch_dev
+    from jeromq_amd import batch
+    n = total - 33
+    base = 127
+    hin = np.frombuffer(splitmix_bytes(n, 4242), dtype=np.uint8)
+    d_in = torch.from_numpy(hin.copy()).to(dev)
+    d_buf = torch.full((base + total + 64,), SENTINEL, dtype=torch.uint8, device=dev)
+    flags = torch.tensor([1], dtype=torch.uint8, device=dev)
+    batch.seal_uniform(d_in, (n + 15) // 16 * 16, d_buf[base:], total, 1, n, subkeys[0], 77, flags8=flags)
+    torch.cuda.synchronize()
+    out = d_buf.cpu().numpy()
+    want = or_curve_encode(hin.tobytes(), 1, 77, 0, PRECOM)
+    assert out[base:base + total].tobytes() == want, f"single {n}-byte frame differs from the oracle"
+    _gaps_untouched(out, [(base, base + total)], 0, len(out))
+
+
+@pytest.mark.parametrize("nout", [SHIFT_TOTAL_MAX, SHIFT_TOTAL_MAX + 1])
+def test_open_uniform_single_frame_at_shift_bound(torch_dev, subkeys, nout):
+    torch, dev = torch_dev
+    from jeromq_amd import _lib, batch
+    p = np.frombuffer(splitmix_bytes(nout, 4343), dtype=np.uint8)
+    body = or_curve_encode(p.tobytes(), 0, 90, 0, PRECOM)
+    d_body = torch.from_numpy(np.frombuffer(body, dtype=np.uint8).copy()).to(dev)
+    base = 127
+    d_buf = torch.full((base + nout + 64,), SENTINEL, dtype=torch.uint8, device=dev)
+    status = torch.full((1,), -1, dtype=torch.int16, device=dev)
+    batch.open_uniform(d_body, len(body), d_buf[base:], nout, 1, len(body), subkeys[0], 89, status)
+    torch.cuda.synchronize()
+    assert int(status.cpu().numpy().view(np.uint16)[0]) & 0xff == _lib.CZ_STATUS_OK
+    out = d_buf.cpu().numpy()
+    assert out[base:base + nout].tobytes() == p.tobytes(), f"single {nout}-byte plaintext differs"
+    _gaps_untouched(out, [(base, base + nout)], 0, len(out))

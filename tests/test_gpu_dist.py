@@ -108,6 +108,12 @@ def test_bench_ws2_rehearsal():
     assert len(lines) == 1, r.stdout[-2000:]
     line = json.loads(lines[0])
     assert line["n_gpus"] == 2 and line["scaling"] == "weak"
+    # the leg runs after the main line is out: pending there, its result on the SCATTER_GATHER line
+    assert line["scatter_gather"]["pending"]
+    sg = [ln for ln in r.stdout.splitlines() if ln.startswith("SCATTER_GATHER ")]
+    assert len(sg) == 1 and r.stdout.index(lines[0]) < r.stdout.index(sg[0]), r.stdout[-2000:]
+    line["scatter_gather"] = json.loads(sg[0][len("SCATTER_GATHER "):])
+    assert line["dist"]["backend"] == "gloo" and line["dist"]["data_backend"] == "gloo"
     # as self-describing as the N = 1 line: slowest-rank roofline with its spread, and the CPU baseline
     roof = line["roofline"]
     assert roof["kernel_ms"] == roof["kernel_ms_max"] == max(p["kernel_ms"] for p in line["per_rank"])
@@ -139,3 +145,4 @@ def test_bench_plain_gpus2_launches_its_own_ranks():
     assert line["dist"]["world_size"] == 2 and line["dist"]["backend"] == "gloo"
     assert line["scatter_gather"]["verified"] and line["seal_open_verify"]["verified"]
     assert line["launcher"].startswith("bench.py --gpus")
+    assert "ranks_exit_status" not in line

@@ -186,6 +186,56 @@ def test_engine_failures_tear_down_one_connection(torch_dev, L):
     assert srv.send(sc[0], b"still fine") == 0
 
 
+def test_engine_remove_conn_drops_its_traffic_and_reuses_the_id(torch_dev, L):
+    """cz_engine_remove_conn (StreamEngine teardown of an attached connection):
+    the removed connection's queued messages leave the flush and its partial input is dropped, the
+    other connections' wire streams and deliveries are unchanged, every call on the removed id fails,
+    and the next add_conn takes the id back with fresh keys and nonces."""
+    from jeromq_amd import _lib
+    from jeromq_amd.engine import CurveBatchEngine
+    rng = np.random.default_rng(11)
+    cli, srv = CurveBatchEngine(arena_bytes=4 << 20), CurveBatchEngine(arena_bytes=4 << 20)
+    cc = [cli.add_connection(_precom(i)) for i in range(3)]
+    sc = [srv.add_connection(_precom(i), as_server=True) for i in range(3)]
+    sent = {i: _messages(rng, 5, 700 + i) for i in range(3)}
+    for k in range(5):                       # interleaved across the three connections
+        for i in range(3):
+            p, fl = sent[i][k]
+            assert cli.send(cc[i], p, more=bool(fl & 1), command=bool(fl & 2)) == 0
+    cli.remove_connection(cc[1])
+    cli.flush_out()
+    for i in (0, 2):
+        assert cli.wire_out(cc[i]) == _oracle_wire(sent[i], _precom(i), 0, 3), f"connection {i}"
+    lib = _lib.lib()
+    assert cli.send(cc[1], b"x") == L.CZ_EINVAL
+    assert lib.cz_engine_remove_conn(cli._h, cc[1]) == L.CZ_EINVAL     # already removed
+    assert lib.cz_engine_remove_conn(cli._h, 99) == L.CZ_EINVAL
+    # server: connection 1 has half a frame buffered when it goes; the others deliver everything
+    w0, w2 = cli.wire_out(cc[0]), cli.wire_out(cc[2])
+    srv.recv(sc[0], w0)
+    srv.recv(sc[1], w0[:77])
+    srv.recv(sc[2], w2)
+    srv.remove_connection(sc[1])
+    srv.flush_in()
+    assert srv.messages_in(sc[0]) == sent[0] and srv.messages_in(sc[2]) == sent[2]
+    assert srv.recv(sc[1], b"\x00") == L.CZ_EINVAL
+    # the id comes back with a new key and new nonces; the neighbours' keys are untouched
+    key = splitmix_bytes(32, 31337)
+    assert cli.add_connection(key, cn_nonce=1000) == cc[1]
+    assert srv.add_connection(key, as_server=True, cn_peer_nonce=999) == sc[1]
+    more = _messages(rng, 4, 880)
+    for p, fl in more:
+        assert cli.send(cc[1], p, more=bool(fl & 1)) == 0
+    assert cli.send(cc[0], b"after") == 0
+    cli.flush_out()
+    w = cli.wire_out(cc[1])
+    assert w == _oracle_wire([(p, fl & 1) for p, fl in more], key, 0, 1000)
+    assert cli.wire_out(cc[0]) == _oracle_wire([(b"after", 0)], _precom(0), 0, 3 + 5)
+    srv.recv(sc[1], w)
+    srv.flush_in()
+    assert srv.messages_in(sc[1]) == [(p, fl & 1) for p, fl in more] and srv.error(sc[1]) == (0, 0)
+
+
 def test_engine_rejects_oversized_message(torch_dev, L):
     from jeromq_amd import _lib
     from jeromq_amd.engine import CurveBatchEngine

@@ -4,8 +4,9 @@ types and the function-table slots the shim calls (indices pinned by static asse
 
 CPU: the shim compiles with -Wall -Wextra -Werror; every Java native the INTEGRATION classes declare
 is exported under its JNI-mangled name; short / null arrays and wrong direct buffers are refused
-before anything is pinned or the library entered; a failed pin releases what was pinned; inputs are
-released with JNI_ABORT and outputs with 0; no JNI call happens inside a critical region.
+before anything is read or the library entered; no Java array is pinned while the library runs
+(inputs copied in with GetByteArrayRegion, outputs copied back with SetByteArrayRegion on success;
+the library entry points are --wrap'ed in the test build to catch a call made under a pin).
 GPU: one MESSAGE box sealed and opened through the jnacl natives (in a VM that hands out copies),
 a uniform batch through GpuCurveBatch over direct buffers, and an engine round trip through
 GpuCurveEngine, all against the oracle."""
@@ -35,8 +36,11 @@ NATIVES = ([JNACL + n for n in ("crypto_1box_1afternm", "crypto_1box_1open_1afte
            + [SECRETBOX + n for n in ("crypto_1secretbox", "crypto_1secretbox_1open")]
            + [BATCH + n for n in ("create", "destroy", "setKeys", "seal", "open", "sealUniform", "openUniform",
                                   "hostAlloc", "hostFree")]
-           + [ENGINE + n for n in ("create", "destroy", "addConn", "msgAlloc", "send", "flushOut", "wireOut",
-                                   "wireIov", "recv", "flushIn", "msgsIn", "msgIn", "connError")])
+           + [ENGINE + n for n in ("create", "destroy", "addConn", "removeConn", "msgAlloc", "send", "flushOut",
+                                   "wireOut", "wireIov", "recv", "flushIn", "msgsIn", "msgIn", "connError")])
+# library entry points the byte[] natives call (interposed in the test build)
+WRAPPED = ("cz_box_afternm", "cz_box_open_afternm", "cz_secretbox", "cz_secretbox_open", "cz_box_beforenm", "cz_box",
+           "cz_box_open", "cz_box_keypair", "cz_engine_add_conn")
 
 vp, i32, i64 = ctypes.c_void_p, ctypes.c_int32, ctypes.c_int64
 
@@ -46,10 +50,13 @@ def shim(tmp_path_factory):
     if not os.path.exists(os.path.join(LIBDIR, "libcurvezmq_mi355x.so")):
         pytest.skip("library not built")
     out = str(tmp_path_factory.mktemp("jni") / "libcz_jni_test.so")
+    # the library calls of the byte[] natives go through the fake's counting wrappers (--wrap), so a
+    # call made while a Java array is pinned is seen
+    wraps = ",".join("--wrap=" + f for f in WRAPPED)
     subprocess.run(["gcc", "-std=c11", "-O2", "-Wall", "-Wextra", "-Werror", "-DCZ_JNI_MIN", "-shared", "-fPIC",
                     "-I" + JNI, "-I" + os.path.join(ROOT, "include"), os.path.join(JNI, "curvezmq_jni.c"),
                     os.path.join(JNI, "fake_jni_env.c"), "-L" + LIBDIR, "-lcurvezmq_mi355x",
-                    "-Wl,-rpath," + LIBDIR, "-o", out], check=True)
+                    "-Wl,-rpath," + LIBDIR, "-Wl," + wraps, "-o", out], check=True)
     L = ctypes.CDLL(out)
     for f in ("fake_env", "fake_byte_array", "fake_int_array", "fake_direct", "fake_heap_buffer", "fake_elem",
               "fake_addr"):
@@ -58,9 +65,12 @@ def shim(tmp_path_factory):
     L.fake_int_array.argtypes = [vp, i32]
     L.fake_direct.argtypes = [vp, i64]
     L.fake_cap.restype = i64
-    for f in ("fake_pins", "fake_releases", "fake_last_mode", "fake_kind", "fake_len", "fake_addr", "fake_cap"):
+    for f in ("fake_pins", "fake_releases", "fake_last_mode", "fake_kind", "fake_len", "fake_addr", "fake_cap",
+              "fake_gets", "fake_sets"):
         getattr(L, f).argtypes = [vp]
     L.fake_elem.argtypes = [vp, i32]
+    L.fake_pin.argtypes = [vp]
+    L.fake_unpin.argtypes = [vp]
     L.fake_fail_new_at.argtypes = [i32]
     for n in NATIVES:
         fn = getattr(L, n)
@@ -91,6 +101,12 @@ class Arr:
 
     def mode(self):
         return self.L.fake_last_mode(self.obj)
+
+    def gets(self):
+        return self.L.fake_gets(self.obj)
+
+    def sets(self):
+        return self.L.fake_sets(self.obj)
 
 
 def _u8(b):
@@ -134,7 +150,7 @@ def _java_sources():
 
 
 def test_java_callers_call_only_declared_natives():
-    """The Java callers (PinnedMsgAllocator, GpuCurveIoHook, GpuCurveMessageBatch, the GPU CURVE
+    """The Java callers (GpuCurveIoHook, GpuCurveMessageBatch, the GPU CURVE
     mechanisms) cannot be compiled here (no JDK): check that every GpuCurveEngine / GpuCurveBatch call
     they make names a native the classes declare -- and so, by the mangling test above, a symbol the
     shim exports -- with the declared number of arguments; that each file's package and class match
@@ -170,8 +186,7 @@ def test_java_callers_call_only_declared_natives():
             assert nargs == natives[(owner, meth)], (path, owner, meth, nargs)
             calls += 1
     assert calls >= 20
-    for f in ("zmq/io/GpuCurveIoHook.java", "zmq/io/mechanism/curve/PinnedMsgAllocator.java",
-              "zmq/io/mechanism/curve/GpuCurveMessageBatch.java", "zmq/io/mechanism/curve/GpuCurveClientMechanism.java",
+    for f in ("zmq/io/GpuCurveIoHook.java", "zmq/io/mechanism/curve/GpuCurveMessageBatch.java", "zmq/io/mechanism/curve/GpuCurveClientMechanism.java",
               "zmq/io/mechanism/curve/GpuCurveServerMechanism.java"):
         assert f in srcs, f
 
@@ -188,8 +203,6 @@ def test_java_callers_use_reference_api_that_exists():
                      "public boolean hasMore()", "public boolean isCommand()", "public void setFlags(int flags)",
                      "public ByteBuffer buf()", "public int size()", "public Msg put(ByteBuffer src, int off, int len)",
                      "public static final int MORE", "public static final int COMMAND"],
-        "msg/MsgAllocator.java": ["Msg allocate(int size);"],
-        "msg/MsgAllocatorHeap.java": ["public class MsgAllocatorHeap implements MsgAllocator"],
         "io/SessionBase.java": ["public SocketBase getSocket()", "public String getEndpoint()"],
         "SocketBase.java": ["public final void eventHandshakeFailedProtocol(String addr, int errno)"],
         "Options.java": ["public final Errno errno", "public boolean asServer"],
@@ -215,9 +228,10 @@ def test_java_callers_use_reference_api_that_exists():
 
 
 @pytest.mark.parametrize("case", ["short_c", "short_m", "short_nonce", "short_key", "mlen_below_32", "null_m"])
-def test_jnacl_length_guards_pin_nothing(shim, case):
+def test_jnacl_length_guards_touch_nothing(shim, case):
     L = shim
     L.fake_reset_log()
+    L.fake_reset_lib_calls()
     mlen = 132
     kw = {"short_c": dict(c_len=131), "short_nonce": dict(n_len=23), "short_key": dict(k_len=31)}.get(case, {})
     c, m, n, k = _box_args(L, mlen=mlen, **kw)
@@ -229,41 +243,59 @@ def test_jnacl_length_guards_pin_nothing(shim, case):
         mlen = 31
     rc = getattr(L, JNACL + "crypto_1box_1afternm")(L.env, None, c.obj, marg, mlen, n.obj, k.obj)
     assert rc == -1
-    assert L.fake_nmodes() == 0 and L.fake_outstanding() == 0
-    assert all(a.pins() == 0 for a in (c, m, n, k))
+    assert L.fake_nmodes() == 0 and L.fake_outstanding() == 0 and L.fake_lib_calls() == 0
+    assert all(a.pins() == 0 and a.gets() == 0 and a.sets() == 0 for a in (c, m, n, k))
 
 
-def test_jnacl_failed_pin_releases_what_it_pinned(shim):
+def test_jnacl_pending_exception_stops_before_the_library(shim):
+    """A VM exception raised while the inputs are copied in (ExceptionCheck) ends the call with -1:
+    the library is not entered and nothing is written back."""
     L = shim
     c, m, n, k = _box_args(L)
-    L.fake_reset_log()
-    L.fake_fail_pin_at(2)          # the nonce's pin fails after c and m were pinned
-    rc = getattr(L, JNACL + "crypto_1box_1afternm")(L.env, None, c.obj, m.obj, 132, n.obj, k.obj)
-    L.fake_reset_log()
-    assert rc == -1 and L.fake_outstanding() == 0
-    assert c.releases() == 1 and m.releases() == 1 and n.pins() == 0 and k.pins() == 0
-    assert c.mode() == JNI_ABORT and m.mode() == JNI_ABORT   # nothing was written: nothing copied back
+    L.fake_reset_refs()
+    L.fake_reset_lib_calls()
+    L.fake_raise()
+    try:
+        rc = getattr(L, JNACL + "crypto_1box_1afternm")(L.env, None, c.obj, m.obj, 132, n.obj, k.obj)
+    finally:
+        L.fake_reset_refs()
+    assert rc == -1 and L.fake_lib_calls() == 0 and c.sets() == 0 and not c.np.any()
 
 
-def test_jnacl_release_modes_and_no_jni_in_critical(shim):
-    """A full call (on a machine without a GPU the library returns -1; on a GPU it seals): the output
-    array is released with 0, every input with JNI_ABORT, each exactly once, in reverse order, and no
-    JNI function is called while the arrays are pinned."""
+def test_jnacl_never_pins_across_the_library_call(shim):
+    """no Java array is pinned while the library runs (a GPU launch + sync): every
+    byte[] native reads its inputs once with GetByteArrayRegion, makes its one library call (counted
+    by the --wrap'ed entry point, which also records whether any array was pinned at that moment),
+    and writes its outputs back with SetByteArrayRegion only when the call succeeded.  Without a GPU
+    the calls return -1 and the output arrays stay untouched; with one they seal.  The detector itself
+    is checked by calling with an array held pinned."""
     L = shim
-    for fn, outs in ((JNACL + "crypto_1box_1afternm", 1), (JNACL + "crypto_1box_1open_1afternm", 1),
-                     (SECRETBOX + "crypto_1secretbox", 1), (SECRETBOX + "crypto_1secretbox_1open", 1)):
+    for fn in (JNACL + "crypto_1box_1afternm", JNACL + "crypto_1box_1open_1afternm",
+               SECRETBOX + "crypto_1secretbox", SECRETBOX + "crypto_1secretbox_1open"):
         c, m, n, k = _box_args(L)
         L.fake_reset_log()
-        getattr(L, fn)(L.env, None, c.obj, m.obj, 132, n.obj, k.obj)
-        assert L.fake_outstanding() == 0 and L.fake_calls_in_critical() == 0
-        assert [a.pins() for a in (c, m, n, k)] == [1, 1, 1, 1]
-        assert [a.releases() for a in (c, m, n, k)] == [1, 1, 1, 1]
-        assert c.mode() == 0 and m.mode() == JNI_ABORT and n.mode() == JNI_ABORT and k.mode() == JNI_ABORT
-        assert [L.fake_mode(i) for i in range(4)] == [JNI_ABORT, JNI_ABORT, JNI_ABORT, 0]   # k, n, m, then c
+        L.fake_reset_lib_calls()
+        rc = getattr(L, fn)(L.env, None, c.obj, m.obj, 132, n.obj, k.obj)
+        assert L.fake_lib_calls() == 1 and L.fake_lib_calls_pinned() == 0, fn
+        assert L.fake_outstanding() == 0 and L.fake_calls_in_critical() == 0 and L.fake_nmodes() == 0
+        assert [a.pins() for a in (c, m, n, k)] == [0, 0, 0, 0]
+        assert [a.gets() for a in (c, m, n, k)] == [0, 1, 1, 1]        # inputs read once, the output never
+        assert c.sets() == (1 if rc == 0 else 0) and m.sets() == n.sets() == k.sets() == 0
     pk, sk = Arr(L, np.zeros(32, np.uint8)), Arr(L, np.zeros(32, np.uint8))
-    L.fake_reset_log()
-    getattr(L, JNACL + "crypto_1box_1keypair")(L.env, None, pk.obj, sk.obj)
-    assert pk.mode() == 0 and sk.mode() == 0 and L.fake_outstanding() == 0
+    L.fake_reset_lib_calls()
+    rc = getattr(L, JNACL + "crypto_1box_1keypair")(L.env, None, pk.obj, sk.obj)
+    assert L.fake_lib_calls() == 1 and L.fake_lib_calls_pinned() == 0 and pk.pins() == sk.pins() == 0
+    assert pk.sets() == sk.sets() == (1 if rc == 0 else 0)
+    # the detector: a call made while some array is pinned is counted as such
+    c, m, n, k = _box_args(L)
+    other = Arr(L, np.zeros(8, np.uint8))
+    L.fake_reset_lib_calls()
+    L.fake_pin(other.obj)
+    try:
+        getattr(L, JNACL + "crypto_1box_1afternm")(L.env, None, c.obj, m.obj, 132, n.obj, k.obj)
+    finally:
+        L.fake_unpin(other.obj)
+    assert L.fake_lib_calls() == 1 and L.fake_lib_calls_pinned() == 1 and L.fake_outstanding() == 0
 
 
 def test_batch_and_engine_refuse_bad_buffers(shim):
@@ -364,7 +396,7 @@ def test_jni_seal_open_through_the_shim(shim):
                 assert getattr(L, fn)(L.env, None, cc.obj, mm.obj, mlen, Arr(L, _u8(bytes.fromhex(v["nonce"]))).obj,
                                       Arr(L, _u8(bytes.fromhex(v["key"]))).obj) == 0, (fn, mlen)
                 assert cc.np.tobytes().hex() == v["c"], (fn, mlen)
-        assert L.fake_outstanding() == 0 and L.fake_calls_in_critical() == 0
+        assert L.fake_outstanding() == 0 and L.fake_calls_in_critical() == 0 and L.fake_lib_calls_pinned() == 0
     finally:
         L.fake_set_copy_mode(0)
 

@@ -59,7 +59,7 @@ def parse():
     ap.add_argument("--plain-stride", type=int, default=0,
                     help="open4k: plaintext slot stride in bytes (0 = the payload stride, 4096)")
     ap.add_argument("--config", default="4k", choices=["4k", "4k_dense", "4k_box", "100b", "zipf", "zipf_open", "zipf_lane", "open4k", "e2e4k",
-                                                          "engine", "nacl", "beforenm"])
+                                                          "engine", "nacl", "beforenm", "jni"])
     ap.add_argument("--frames", type=int, default=FRAMES)
     ap.add_argument("--chunk-frames", type=int, default=16384, help="e2e4k: frames per pipeline chunk")
     ap.add_argument("--no-cpu-baseline", action="store_true")
@@ -949,6 +949,28 @@ def hbm_copy_ceiling(dev, nbytes=1 << 31, reps=10):
     return k, t
 
 
+def pmc_freshness(pmc, lib_path=None):
+    """Whether the committed counter entry belongs to the library loaded now: sha256 of the machine
+    code of the kernels it was measured on (jeromq_amd.build.kernel_code_sha256, recorded by
+    tools/traffic_update.py / valu_update.py) against the same kernels in the loaded library.
+    {"traffic_stale": bool | None, "valu_stale": ..., "kernel_sha256": loaded}; None = the entry
+    carries no sha (measured before round 6) or no counters."""
+    from jeromq_amd.build import kernel_code_sha256
+    lib_path = lib_path or _lib.LIB_PATH
+    out = {}
+    for part, kern_key in (("traffic", "kernels"), ("valu", "valu_kernels")):
+        kernels = pmc.get(kern_key) or pmc.get("kernels")
+        want = pmc.get(f"{part}_kernel_sha256")
+        have = None
+        try:
+            have = kernel_code_sha256(lib_path, kernels) if kernels else None
+        except Exception as e:  # noqa: BLE001 -- a missing tool leaves the question open, never fails the bench
+            out[f"{part}_check_error"] = str(e)[:200]
+        out[f"{part}_stale"] = None if not want or have is None else want != have
+        out[f"{part}_kernel_sha256_loaded"] = have
+    return out
+
+
 def valu_roofline(pmc, kernel_s):
     n = pmc.get("valu_insts_per_launch")
     if not n:
@@ -1041,8 +1063,39 @@ def roundtrip_leg(wl, world, steps):
             "payload_GiBps": round(total / elapsed / 2**30, 3), "verified": bool(ok)}
 
 
+def jni_host(args):
+    """The host path timed THROUGH the JNI shim (north star: the end-to-end rate including the JNI
+    pinned-buffer copies): tools/bin/jni_bench (jni/jni_bench.c, built by __graft_entry__.build)
+    drives jni/curvezmq_jni.c over the fake JNIEnv -- GpuCurveBatch.sealUniform / openUniform on
+    hostAlloc direct buffers at 4 KiB (2^16 .. --frames) and 100 B, the jnacl crypto_box_afternm per
+    message, the GpuCurveEngine loop of GpuCurveIoHook over 1024 connections -- each beside the plain
+    C-ABI on the same buffers.  Run as a child process: this one never touches the GPU.  `value` =
+    the 4 KiB seal at the largest batch through the shim, payload GiB/s (pinned host in and out)."""
+    import subprocess
+    exe = os.path.join(ROOT, "tools", "bin", "jni_bench")
+    if not os.path.exists(exe):
+        raise SystemExit(f"{exe} is missing: run __graft_entry__.build() (gcc, the JNI shim over a fake JNIEnv)")
+    r = subprocess.run([exe, str(args.frames), str(max(args.steps // 6, 3))], capture_output=True, text=True,
+                       timeout=1200)
+    sys.stderr.write(r.stderr)
+    if r.returncode != 0:
+        print(f"jni_bench failed (exit {r.returncode})", file=sys.stderr)
+        return r.returncode or 1
+    line = json.loads(r.stdout.strip().splitlines()[-1])
+    big = max((u for u in line["uniform"] if u["payload_bytes"] == 4096), key=lambda u: u["frames"])
+    line.update({"value": big["seal_GiBps"], "unit": "GiB/s", "n_gpus": 1, "higher_is_better": True,
+                 "verified": all(u["verified"] for u in line["uniform"]) and all(x["verified"] for x in line["jnacl"])
+                 and line["engine"]["verified"],
+                 "config": {"workload": f"{big['frames']} x 4 KiB frames, pinned host buffers through "
+                                        "GpuCurveBatch.sealUniform (JNI shim, fake JNIEnv)", "frames": big["frames"]}})
+    print(json.dumps(line), flush=True)
+    return 0 if line["verified"] else 1
+
+
 def main():
     args = parse()
+    if args.config == "jni":
+        sys.exit(jni_host(args))
     if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
         sys.exit(launch_ranks(args.gpus, sys.argv[1:]))
     world, rank, local = setup_dist(args)
@@ -1112,6 +1165,7 @@ def main():
     pmc_key = key_from_args(args)
     pmc = load_pmc(pmc_key)
     traffic = pmc.get("hbm_bytes_per_launch")
+    pmc_build = pmc_freshness(pmc)
 
     want_leg = world > 1 and args.config == "4k" and not args.no_scatter
 
@@ -1174,7 +1228,10 @@ def main():
                          "torch_copy_GBps": torch_copy_gbs,
                          "pmc_key": pmc_key,
                          "alg_bytes_per_launch": alg_bytes,
-                         "valu": valu_roofline(pmc, slow_kernel_s)},
+                         "valu": valu_roofline(pmc, slow_kernel_s),
+                         # traffic / valu are committed rocprofv3 counts (profiles/pmc_traffic.json):
+                         # stale when the loaded library's code of the measured kernels differs
+                         "pmc_build": pmc_build},
             "cpu_baseline": cpu,
         }
         if rtl is not None:

@@ -85,6 +85,50 @@ def device_code_objects(so_path, arch=ARCH):
     return cos
 
 
+def _elf_functions(co):
+    """(name, machine code bytes) of every FUNC symbol of one ELF64 code object"""
+    (shoff,) = struct.unpack_from("<Q", co, 0x28)
+    shentsize, shnum = struct.unpack_from("<HH", co, 0x3A)
+    secs = [struct.unpack_from("<IIQQQQIIQQ", co, shoff + k * shentsize) for k in range(shnum)]
+    out = []
+    for sec in secs:
+        if sec[1] != 2:                      # SHT_SYMTAB
+            continue
+        strtab = secs[sec[6]]
+        for k in range(sec[5] // 24):        # Elf64_Sym: name, info, other, shndx, value, size
+            name_off, info, _, shndx, value, size = struct.unpack_from("<IBBHQQ", co, sec[4] + 24 * k)
+            if info & 0xF != 2 or not size or shndx >= len(secs):   # STT_FUNC with code
+                continue
+            end = co.index(b"\0", strtab[4] + name_off)
+            name = co[strtab[4] + name_off:end].decode()
+            text = secs[shndx]
+            start = text[4] + (value - text[3])   # file offset = section offset + (address - section address)
+            out.append((name, bytes(co[start:start + size])))
+    return out
+
+
+def kernel_code_sha256(so_path, kernels, arch=ARCH):
+    """sha256 over the machine code of `kernels` (demangled names as rocprofv3 prints them, e.g.
+    "k_seal_uniform<1, true, 0>") in the library's gfx950 code objects: what ties a committed PMC
+    count (profiles/pmc_traffic.json) to the build it was measured on -- another kernel's change
+    leaves it alone, a change to one of these kernels makes it stale.  None if a kernel is absent."""
+    import hashlib
+    funcs = [f for co in device_code_objects(so_path, arch) for f in _elf_functions(co)]
+    names = [n for n, _ in funcs]
+    filt = shutil.which("c++filt") or shutil.which("llvm-cxxfilt")
+    dem = subprocess.run([filt], input="\n".join(names), capture_output=True, text=True, check=True).stdout.split("\n")
+    code = {}
+    for (n, b), d in zip(funcs, dem):
+        d = d.replace("(anonymous namespace)::", "")
+        code.setdefault(d.split("(")[0].replace("void ", "", 1).strip(), b)
+    h = hashlib.sha256()
+    for k in sorted(kernels):
+        if k not in code:
+            return None
+        h.update(k.encode() + b"\0" + code[k])
+    return h.hexdigest()
+
+
 def disassemble(code_object, arch=ARCH):
     """llvm-objdump listing of one code object, reduced to instruction lines (no labels or
     encoding comments), the form tools/isa_store_hazard.scan reads."""
@@ -165,6 +209,28 @@ def build_library(force=False, verbose=True, sources=None, lib=None, src_dir=Non
     finally:
         shutil.rmtree(objdir, ignore_errors=True)
     return lib
+
+
+JNI_DIR = os.path.join(ROOT, "jni")
+JNI_BENCH = os.path.join(ROOT, "tools", "bin", "jni_bench")
+# the library entry points jni/fake_jni_env.c interposes (tests/test_jni_shim.py links the same list)
+JNI_WRAPPED = ("cz_box_afternm", "cz_box_open_afternm", "cz_secretbox", "cz_secretbox_open", "cz_box_beforenm", "cz_box",
+               "cz_box_open", "cz_box_keypair", "cz_engine_add_conn")
+
+
+def build_jni_bench(lib=PRODUCT_LIB, out=JNI_BENCH):
+    """tools/bin/jni_bench (bench.py --config jni): the JNI shim, the fake JNIEnv and the driver
+    jni/jni_bench.c against the product library, with an $ORIGIN-relative rpath so the binary runs
+    from the repository copy on the GPU box."""
+    os.makedirs(os.path.dirname(out), exist_ok=True)
+    rel = os.path.relpath(os.path.dirname(lib), os.path.dirname(out))
+    cmd = ["gcc", "-std=c11", "-O2", "-Wall", "-Wextra", "-Werror", "-DCZ_JNI_MIN", "-I" + JNI_DIR,
+           "-I" + os.path.join(ROOT, "include"), os.path.join(JNI_DIR, "jni_bench.c"),
+           os.path.join(JNI_DIR, "curvezmq_jni.c"), os.path.join(JNI_DIR, "fake_jni_env.c"),
+           "-L" + os.path.dirname(lib), "-lcurvezmq_mi355x", "-Wl,-rpath,$ORIGIN/" + rel,
+           "-Wl," + ",".join("--wrap=" + f for f in JNI_WRAPPED), "-o", out]
+    subprocess.check_call(cmd)
+    return out
 
 
 if __name__ == "__main__":

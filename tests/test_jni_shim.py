@@ -39,8 +39,7 @@ NATIVES = ([JNACL + n for n in ("crypto_1box_1afternm", "crypto_1box_1open_1afte
            + [ENGINE + n for n in ("create", "destroy", "addConn", "removeConn", "msgAlloc", "send", "flushOut",
                                    "wireOut", "wireIov", "recv", "flushIn", "msgsIn", "msgIn", "connError")])
 # library entry points the byte[] natives call (interposed in the test build)
-WRAPPED = ("cz_box_afternm", "cz_box_open_afternm", "cz_secretbox", "cz_secretbox_open", "cz_box_beforenm", "cz_box",
-           "cz_box_open", "cz_box_keypair", "cz_engine_add_conn")
+from jeromq_amd.build import JNI_WRAPPED as WRAPPED  # noqa: E402
 
 vp, i32, i64 = ctypes.c_void_p, ctypes.c_int32, ctypes.c_int64
 

@@ -20,6 +20,9 @@ KERNELS = {"4k": ("k_seal_uniform",), "100b": ("k_seal_uniform",), "open4k": ("k
            "zipf_open": ("k_open_segments", "k_open_combine"),
            "4k_dense": ("k_seal_uniform",)}
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+from jeromq_amd.build import PRODUCT_LIB, kernel_code_sha256  # noqa: E402
+LIB = os.environ.get("CZ_LIB", PRODUCT_LIB)   # the library the passes ran (A/B builds set CZ_LIB)
 path = os.path.join(ROOT, "profiles", "pmc_traffic.json")
 data = json.load(open(path)) if os.path.exists(path) else {}
 
@@ -42,7 +45,11 @@ for cfg in cfgs:
         continue
     fb = sum(v * 1024 * 2 for v in fetch.values())
     wb = sum(v * 1024 for v in write.values())
-    data[cfg] = {"hbm_bytes_per_launch": round(fb + wb), "fetch_bytes": round(fb), "write_bytes": round(wb),
-                 "kernels": sorted(fetch), "source": f"tools/gpu_traffic.sh {cfg} (rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE)"}
+    entry = data.setdefault(cfg, {})
+    entry.update({"hbm_bytes_per_launch": round(fb + wb), "fetch_bytes": round(fb), "write_bytes": round(wb),
+                  "kernels": sorted(fetch), "source": f"tools/gpu_traffic.sh {cfg} (rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE)",
+                  # the machine code these counts belong to: bench.py marks them stale when the loaded
+                  # library's code of these kernels differs
+                  "traffic_kernel_sha256": kernel_code_sha256(LIB, sorted(fetch))})
     print(cfg, data[cfg])
 json.dump(data, open(path, "w"), indent=1)

@@ -21,6 +21,9 @@ KERNELS = {"4k": ("k_seal_uniform",), "100b": ("k_seal_uniform",), "open4k": ("k
            "zipf_open": ("k_open_segments", "k_open_combine"),
            "4k_dense": ("k_seal_uniform",)}
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+from jeromq_amd.build import PRODUCT_LIB, kernel_code_sha256  # noqa: E402
+LIB = os.environ.get("CZ_LIB", PRODUCT_LIB)   # the library the passes ran (A/B builds set CZ_LIB)
 path = os.path.join(ROOT, "profiles", "pmc_traffic.json")
 data = json.load(open(path)) if os.path.exists(path) else {}
 
@@ -52,6 +55,7 @@ for cfg in cfgs:
                   "lds_insts_per_launch": round(tot("SQ_INSTS_LDS")),
                   "profiled_clock_ghz": round(med[dom].get("GRBM_GUI_ACTIVE", 0.0) / 8 / t / 1e9, 3),
                   "profiled_kernel_ms": round(t * 1e3, 4),
-                  "valu_source": f"tools/gpu_valu.sh {cfg} (rocprofv3 --pmc SQ_INSTS_VALU ... GRBM_GUI_ACTIVE)"})
+                  "valu_source": f"tools/gpu_valu.sh {cfg} (rocprofv3 --pmc SQ_INSTS_VALU ... GRBM_GUI_ACTIVE)",
+                  "valu_kernels": sorted(med), "valu_kernel_sha256": kernel_code_sha256(LIB, sorted(med))})
     print(cfg, {k: entry[k] for k in entry if k.startswith(("valu", "salu", "lds", "profiled"))})
 json.dump(data, open(path, "w"), indent=1)

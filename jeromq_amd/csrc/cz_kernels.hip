@@ -1004,36 +1004,6 @@ __device__ __forceinline__ void carry_window(u32 C[16], const u32 Cur[32], const
     }
 }
 
-// Half carry (round 6, open_frame<CARRY = 2>): the same phase-sorted waves, but each aligned line
-// is loaded once and only its upper half (dwords 16..31) is carried.  With the body's dword phase
-// s = 16 p + t (t < 16, wave-uniform), block b's window is dwords [s + 16 b, s + 16 b + 16] of the
-// line grid: the blocks pair up per aligned line L as (straddler, inner) -- the straddler's window
-// is line L-1's dwords [16 + t, 32) and line L's [0, t], the inner block's is line L's [t, t + 16].
-// Over X = Kup[0..15] ++ New[0..31] (Kup = line L-1's upper half) both are X[BASE + t .. + 16]:
-// BASE 0 for the straddler, 16 for the inner block.  48 live dwords instead of Cur + Nxt's 64.
-template <int T, int BASE>
-__device__ __forceinline__ void carry_half_s(u32 C[16], const u32 Kup[16], const u32 New[32], u32 ina)
-{
-#pragma unroll
-    for (int q = 0; q < 16; q++) {
-        const int lo = BASE + T + q, hi = lo + 1;
-        const u32 vlo = lo < 16 ? Kup[lo & 15] : New[(lo - 16) & 31];
-        const u32 vhi = hi < 16 ? Kup[hi & 15] : New[(hi - 16) & 31];
-        C[q] = funnel(vhi, vlo, ina);
-    }
-}
-template <int BASE>
-__device__ __forceinline__ void carry_half(u32 C[16], const u32 Kup[16], const u32 New[32], u32 t, u32 ina)
-{
-    switch (t) {
-#define CZ_CH(T) case T: carry_half_s<T, BASE>(C, Kup, New, ina); break;
-        CZ_CH(0) CZ_CH(1) CZ_CH(2) CZ_CH(3) CZ_CH(4) CZ_CH(5) CZ_CH(6) CZ_CH(7)
-        CZ_CH(8) CZ_CH(9) CZ_CH(10) CZ_CH(11) CZ_CH(12) CZ_CH(13) CZ_CH(14)
-        default: carry_half_s<15, BASE>(C, Kup, New, ina); break;
-#undef CZ_CH
-    }
-}
-
 // --------------------------------------------------------------------------
 // OPEN one frame.  Returns a CZ_STATUS_* code; the emitter receives the output:
 //   MODE_ZMQ : in = MESSAGE body (size bytes), output = payload (size - 33 bytes);
@@ -1052,7 +1022,7 @@ __device__ __forceinline__ void carry_half(u32 C[16], const u32 Kup[16], const u
 // the body never reads past the dword holding its last byte (a dword cannot cross a page) nor
 // below the body's first dword (the buffer base is dword-aligned).
 template <int MODE, bool AL, class EM, bool PAIR = false, bool UN0 = false, bool LAZY = true, int INA = 16,
-          int CARRY = 0>
+          bool CARRY = false>
 __device__ __forceinline__ u32 open_frame(const uint8_t *__restrict__ in, u32 size, const u32 key[8],
                                           bool check_floor, long long floor, u32 *flags_out, u64 *nonce_out,
                                           u64 nacl_counter, EM &em)
@@ -1285,61 +1255,7 @@ __device__ __forceinline__ u32 open_frame(const uint8_t *__restrict__ in, u32 si
                 C[k] = L1[k];  // (loaded with the rest of line 0, above)
             open_block(1, true);
             blk = 2;
-            if constexpr (CARRY == 2) {
-                static_assert(INA != 16, "carry-line input is for bodies off 16-byte alignment");
-                // half carry (see carry_half): the caller sorted frames so that every lane of the wave
-                // has the same line phase s = 16 p + t
-                const uint8_t *lb = reinterpret_cast<const uint8_t *>((uintptr_t)in4 & ~(uintptr_t)127);
-                const u32 sd = __builtin_amdgcn_readfirstlane(((u32)(uintptr_t)in4 & 127u) >> 2);
-                const u32 t = sd & 15u;
-                const bool p = sd >= 16u;
-                u32 Kup[16], New[32];
-                auto load_line = [&](const uint8_t *q) {
-#pragma unroll
-                    for (int c = 0; c < 8; c++) {
-                        const uint4 v = *reinterpret_cast<const uint4 *>(q + 16 * c);
-                        New[4 * c] = v.x; New[4 * c + 1] = v.y; New[4 * c + 2] = v.z; New[4 * c + 3] = v.w;
-                    }
-                };
-                // blocks 0 and 1 are done (body line 0, above).  p: block 2L - 2 straddles lines L - 1 and
-                // L, block 2L - 1 is inside L.  !p: block 2L - 1 straddles, block 2L is inside.  Line 1
-                // holds a body byte of every block it serves, so it is mapped.
-                load_line(lb + 128);
-                u32 L = 1;
-                if (!p && 2u < nfull) {
-                    // line 1's inner block 2 (its straddler, block 1, is done)
-                    open_block_f(2u, true, true, nullptr, [&] {
-                        __builtin_amdgcn_sched_barrier(0);
-                        carry_half<16>(C, Kup, New, t, ina);
-                    });
-                    blk = 3;
-                }
-#pragma unroll
-                for (int q = 0; q < 16; q++)
-                    Kup[q] = New[16 + q];
-                // line L + 1 serves blocks b0 = 2L + 1 - p and b0 + 1 (both full: b0 + 1 < nfull); it holds
-                // a body byte of b0 + 1, so it is mapped
-                for (L = 2; 2u * L - (p ? 1u : 0u) < nfull; L++) {
-                    const u32 b0 = 2u * L - (p ? 2u : 1u);
-                    if (!p && b0 != blk)
-                        break;  // (block 2 was not full)
-                    load_line(lb + 128u * L);
-                    __builtin_amdgcn_sched_barrier(0);
-                    open_block_f(b0, true, true, nullptr, [&] {
-                        __builtin_amdgcn_sched_barrier(0);
-                        carry_half<0>(C, Kup, New, t, ina);
-                    });
-                    open_block_f(b0 + 1u, true, false, nullptr, [&] {
-                        __builtin_amdgcn_sched_barrier(0);
-                        carry_half<16>(C, Kup, New, t, ina);
-                    });
-#pragma unroll
-                    for (int q = 0; q < 16; q++)
-                        Kup[q] = New[16 + q];
-                    blk = b0 + 2u;
-                }
-            }
-            if constexpr (CARRY == 1) {
+            if constexpr (CARRY) {
                 static_assert(INA != 16, "carry-line input is for bodies off 16-byte alignment");
                 // the caller sorted frames so that every lane of the wave has the same line phase
                 const uint8_t *lb = reinterpret_cast<const uint8_t *>((uintptr_t)in4 & ~(uintptr_t)127);
@@ -1372,7 +1288,7 @@ __device__ __forceinline__ u32 open_frame(const uint8_t *__restrict__ in, u32 si
                     blk = 2u * k + 2u;
                 }
             }
-            for (u32 k = 1; CARRY == 0 && 2u * k + 1u < nfull; k++) {
+            for (u32 k = 1; !CARRY && 2u * k + 1u < nfull; k++) {
                 u32 M[32];
                 if constexpr (INA == 1) {
                     // 8 loads from the dword-aligned line below and the dword after it, funnelled
@@ -2921,8 +2837,8 @@ __global__ __launch_bounds__(BLOCK) CZ_OCC CZ_OPEN_UNI_OCC void k_open_uniform(c
 // aligned line of a body once and carries it into the next pair.  Plaintext slot j of the wave is
 // out + (first + P j) * out_stride, EmitLines with a lane stride of P * out_stride.  nwaves = the
 // number of whole blocks x P; the frames after them go to k_open_uniform (prev0 = 1).
-template <int INA, int CM>
-__device__ __forceinline__ void open_uniform_carry_body(
+template <int INA>
+__global__ __launch_bounds__(BLOCK) CZ_OPEN_CARRY_OCC void k_open_uniform_carry(
     const uint8_t *__restrict__ in, uint64_t in_stride, uint8_t *__restrict__ out, uint64_t out_stride, uint32_t nwaves,
     uint32_t P, uint32_t size, const uint8_t *__restrict__ subkey, uint64_t floor0, int check,
     uint16_t *__restrict__ status, int allow_un0)
@@ -2956,33 +2872,12 @@ __device__ __forceinline__ void open_uniform_carry_body(
     u64 nonce = 0;
     u32 st;
     if (un0)
-        st = open_frame<MODE_ZMQ, true, EmL, true, true, true, INA, CM>(src, size, key, check != 0, floor, &fl,
+        st = open_frame<MODE_ZMQ, true, EmL, true, true, true, INA, true>(src, size, key, check != 0, floor, &fl,
                                                                             &nonce, 0, em);
     else
-        st = open_frame<MODE_ZMQ, true, EmL, true, false, true, INA, CM>(src, size, key, check != 0, floor, &fl,
+        st = open_frame<MODE_ZMQ, true, EmL, true, false, true, INA, true>(src, size, key, check != 0, floor, &fl,
                                                                              &nonce, 0, em);
     status[i] = (uint16_t)(st | (st == CZ_STATUS_OK ? (fl << 8) : 0u));
-}
-
-// CM 1: two whole lines carried (64 VGPRs, 2 waves per SIMD); CM 2 (round 6): the upper half-line
-// carried (carry_half), built for 3 waves per SIMD like k_open_uniform
-template <int INA>
-__global__ __launch_bounds__(BLOCK) CZ_OPEN_CARRY_OCC void k_open_uniform_carry(
-    const uint8_t *__restrict__ in, uint64_t in_stride, uint8_t *__restrict__ out, uint64_t out_stride, uint32_t nwaves,
-    uint32_t P, uint32_t size, const uint8_t *__restrict__ subkey, uint64_t floor0, int check,
-    uint16_t *__restrict__ status, int allow_un0)
-{
-    open_uniform_carry_body<INA, 1>(in, in_stride, out, out_stride, nwaves, P, size, subkey, floor0, check, status,
-                                    allow_un0);
-}
-template <int INA>
-__global__ __launch_bounds__(BLOCK) CZ_OPEN_UNI_OCC void k_open_uniform_carry_half(
-    const uint8_t *__restrict__ in, uint64_t in_stride, uint8_t *__restrict__ out, uint64_t out_stride, uint32_t nwaves,
-    uint32_t P, uint32_t size, const uint8_t *__restrict__ subkey, uint64_t floor0, int check,
-    uint16_t *__restrict__ status, int allow_un0)
-{
-    open_uniform_carry_body<INA, 2>(in, in_stride, out, out_stride, nwaves, P, size, subkey, floor0, check, status,
-                                    allow_un0);
 }
 
 #if CZ_KPART_HAS(3)
@@ -3885,8 +3780,7 @@ hipError_t czk_open_uniform(const void *in, uint64_t in_stride, void *out, uint6
     // (INA 1 -- any byte offset -- measured 1.3% slower with carried lines at 2 waves per SIMD than
     // the straddling loads at 3, so only 8-byte aligned bodies take it: +2.6%)
     // (cz_tune("open_carry", 2): INA 1 too, A/B only)
-    // (cz_tune("open_carry", 3): the half-line carry at 3 waves per SIMD, INA 8 and 1, k_open_uniform_carry_half)
-    if (g_pair && st_out == ST_LINES && (ina == 8 || (ina == 1 && g_open_carry >= 2)) && g_open_ina && g_open_carry &&
+    if (g_pair && st_out == ST_LINES && (ina == 8 || (ina == 1 && g_open_carry == 2)) && g_open_ina && g_open_carry &&
         nout >= 256u) {
         // phase-sorted waves with carried aligned lines (k_open_uniform_carry): whole blocks of 64 P
         // frames, P = the period of the bodies' line phase; the rest through k_open_uniform
@@ -3901,15 +3795,7 @@ hipError_t czk_open_uniform(const void *in, uint64_t in_stride, void *out, uint6
         if (blocks > 0 && 64ull * P * out_stride < (1ull << 31)) {
             const uint32_t nwaves = (uint32_t)(blocks * P);
             const dim3 cgrid((nwaves + WAVES - 1) / WAVES);
-            if (g_open_carry == 3 && ina == 8)
-                hipLaunchKernelGGL((k_open_uniform_carry_half<8>), cgrid, dim3(BLOCK), WAVES * LINE_LDS_BYTES, s,
-                                   (const uint8_t *)in, in_stride, (uint8_t *)out, out_stride, nwaves, P, size,
-                                   (const uint8_t *)subkey, floor0, check, status, g_un0);
-            else if (g_open_carry == 3)
-                hipLaunchKernelGGL((k_open_uniform_carry_half<1>), cgrid, dim3(BLOCK), WAVES * LINE_LDS_BYTES, s,
-                                   (const uint8_t *)in, in_stride, (uint8_t *)out, out_stride, nwaves, P, size,
-                                   (const uint8_t *)subkey, floor0, check, status, g_un0);
-            else if (ina == 8)
+            if (ina == 8)
                 hipLaunchKernelGGL((k_open_uniform_carry<8>), cgrid, dim3(BLOCK), WAVES * LINE_LDS_BYTES, s,
                                    (const uint8_t *)in, in_stride, (uint8_t *)out, out_stride, nwaves, P, size,
                                    (const uint8_t *)subkey, floor0, check, status, g_un0);
@@ -4085,7 +3971,7 @@ int czk_tune(const char *key, int value)
     }
     if (__builtin_strcmp(key, "open_carry") == 0) {
         int old = g_open_carry;
-        g_open_carry = value < 0 ? 0 : value > 3 ? 3 : value;
+        g_open_carry = value < 0 ? 0 : value > 2 ? 2 : value;
         return old;
     }
     if (__builtin_strcmp(key, "shift16") == 0) {

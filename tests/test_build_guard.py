@@ -3,7 +3,8 @@
 jeromq_amd/build.py refuses CZ_EXTRA_FLAGS for the product output (jeromq_amd/libcurvezmq_mi355x.so),
 so a variable left set on a build box cannot ship an A/B variant or a wrong-output diagnostic; A/B
 builds name another output with CZ_LIB_OUT.  The one diagnostic hook left in the kernels
-(cz_diag.h, CZ_DIAG_NOSTORE_ALL) also #errors when compiled with -DCZ_PRODUCT_BUILD."""
+(cz_diag.h, CZ_DIAG_NOSTORE_ALL) and the round-6 clock stamps (CZ_DIAG_CLOCK, tools/clock_stamp.py) also
+#error when compiled with -DCZ_PRODUCT_BUILD."""
 import os
 import subprocess
 
@@ -30,7 +31,8 @@ def test_ab_builds_take_their_flags(tmp_path):
 
 
 @pytest.mark.parametrize("defs, ok", [(["-DCZ_PRODUCT_BUILD"], True), (["-DCZ_DIAG_NOSTORE_ALL"], True),
-                                      (["-DCZ_PRODUCT_BUILD", "-DCZ_DIAG_NOSTORE_ALL"], False)])
+                                      (["-DCZ_PRODUCT_BUILD", "-DCZ_DIAG_NOSTORE_ALL"], False),
+                                      (["-DCZ_DIAG_CLOCK"], True), (["-DCZ_PRODUCT_BUILD", "-DCZ_DIAG_CLOCK"], False)])
 def test_diag_header_refuses_product_builds(tmp_path, defs, ok):
     src = tmp_path / "d.cpp"
     src.write_text('#include "cz_diag.h"\nstruct V { unsigned x, w; };\n'

@@ -976,10 +976,18 @@ def valu_roofline(pmc, kernel_s):
     if not n:
         return None
     g = n / kernel_s / 1e9
-    return {"insts_per_launch": n, "achieved": round(g, 1), "peak": VALU_PEAK_G, "unit": "G wave-instr/s",
-            "frac": round(g / VALU_PEAK_G, 4),
-            "floor_ms_at_2.4GHz": round(n / (VALU_PEAK_G * 1e9) * 1e3, 4),
-            "source": pmc.get("valu_source")}
+    out = {"insts_per_launch": n, "achieved": round(g, 1), "peak": VALU_PEAK_G, "unit": "G wave-instr/s",
+           "frac": round(g / VALU_PEAK_G, 4),
+           "floor_ms_at_2.4GHz": round(n / (VALU_PEAK_G * 1e9) * 1e3, 4),
+           "source": pmc.get("valu_source")}
+    clk = pmc.get("stamped_clock_ghz")
+    if clk:
+        # the issue roof at the clock the kernel really runs at (in-kernel s_memtime stamps, unprofiled):
+        # the fraction of that clock's cycles the SIMDs spend issuing VALU
+        out["stamped_clock_ghz"] = clk
+        out["frac_at_clock"] = round(n * 4 / 1024 / (clk * 1e9) / kernel_s, 4)
+        out["clock_source"] = pmc.get("stamped_clock_source")
+    return out
 
 
 def scatter_leg(wl, world, rank, dev):

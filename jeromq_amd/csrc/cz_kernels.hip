@@ -2063,12 +2063,8 @@ __device__ __forceinline__ u32 seal_seg_bytes(u32 mlen, u32 b0, u32 bend)
 // any byte offset, read from the dword boundary at or above it with the funnel shift sh).
 template <bool AL, class EM, bool PAIR = false, int INA = 16>
 __device__ __forceinline__ void seal_segment(const uint8_t *__restrict__ in0, u32 n, u32 flags, u64 counter, const u32 key[8], u32 b0,
-                             u32 b1, u32 *__restrict__ work, u32 part, EM &em, u32 nrun = 0)
+                             u32 b1, u32 *__restrict__ rec, EM &em, u32 nrun = 0)
 {
-    // the partial record of a split frame's segment (part != ~0); its address is formed where it is
-    // used (work is kernel-uniform, part one VGPR), not carried as a 64-bit pointer through the blocks
-    const bool has_rec = part != 0xffffffffu;
-    auto recp = [&]() -> u32 * { return work + 16ull * part; };
     static_assert(INA == 16 || AL, "INA 8/1 take the AL code paths");
     const u32 ina_a = INA == 1 ? (u32)(uintptr_t)in0 & 3u : 0u;
     const u32 ina_d = (4u - ina_a) & 3u;
@@ -2103,7 +2099,7 @@ __device__ __forceinline__ void seal_segment(const uint8_t *__restrict__ in0, u3
     // bytes from `in`.  A payload of 0..2 bytes at an odd offset is shorter than d = -in0 & 3 and
     // lies wholly in P[-1] (pm1): no load may read past it (n - d would wrap to ~2^64, and the pair
     // loop would then read up to 128 bytes past the payload).
-    const u32 inlen = n > ina_d ? n - ina_d : 0u;  // (frames are below 2^31 bytes: 32-bit offsets)
+    const u64 inlen = n > ina_d ? (u64)(n - ina_d) : 0ull;
     u32 n0, n1;
     counter_nonce(counter, n0, n1);
     u32 x[16], C[16];
@@ -2111,17 +2107,6 @@ __device__ __forceinline__ void seal_segment(const uint8_t *__restrict__ in0, u3
     Poly P;
     poly_init(P, x[0], x[1], x[2], x[3], x[4], x[5], x[6], x[7]);
     u32 mpoly = 0;
-    // Cooperative emitters (the 3-wave lines kernel, where every VGPR counts): the pad -- keystream
-    // words 4..7 -- is used only at the very end, so it waits in memory during the blocks: in the
-    // record of a split frame's segment 0 (where the combine reads it), else in the frame's tag slot,
-    // which the line flushes leave to tag() and which this lane alone writes.
-    constexpr bool PARK = EM::cooperative;
-    if constexpr (PARK) {
-        if (b0 == 0) {
-            u32 *pp = has_rec ? recp() + 12 : reinterpret_cast<u32 *>(em.mine + 16);
-            *reinterpret_cast<uint4 *>(pp) = make_uint4(P.p0, P.p1, P.p2, P.p3);
-        }
-    }
 
     // box block blk from its 17-dword window W = P[16blk-9 .. 16blk+7] (P[-1] = flags << 24);
     // own = false: a block past this lane's segment, run only to keep the wave in step
@@ -2178,8 +2163,8 @@ __device__ __forceinline__ void seal_segment(const uint8_t *__restrict__ in0, u3
             u32 L[32];
 #pragma unroll
             for (int c = 0; c < 8; c++) {
-                const int o = (int)(64u * b0) - 64 + 16 * c;
-                V4 v = (o < 0) ? zero4() : ldP(ln + 16 * c, (u32)o < inlen ? inlen - (u32)o : 0u);
+                const long o = (long)(64u * b0) - 64 + 16 * c;
+                V4 v = (o < 0) ? zero4() : ldP(ln + 16 * c, (u64)o < inlen ? inlen - (u64)o : 0);
                 L[4 * c] = v.x; L[4 * c + 1] = v.y; L[4 * c + 2] = v.z; L[4 * c + 3] = v.w;
             }
             if (b0 == 0)
@@ -2204,7 +2189,7 @@ __device__ __forceinline__ void seal_segment(const uint8_t *__restrict__ in0, u3
         for (u32 q = q0; q < run; q += 2u) {
             const u32 blk = b0 + q;
             const uint8_t *src = in + 64u * blk;
-            const u32 o = 64u * blk;
+            const u64 o = 64ull * blk;
             u32 L[32];
             if (o + 128u <= inlen) {
 #pragma unroll
@@ -2215,7 +2200,7 @@ __device__ __forceinline__ void seal_segment(const uint8_t *__restrict__ in0, u3
             } else {
 #pragma unroll
                 for (int c = 0; c < 8; c++) {
-                    V4 v = ldP(src + 16 * c, inlen > o + 16u * c ? inlen - o - 16u * c : 0u);
+                    V4 v = ldP(src + 16 * c, inlen > o + 16u * c ? inlen - o - 16u * c : 0);
                     L[4 * c] = v.x; L[4 * c + 1] = v.y; L[4 * c + 2] = v.z; L[4 * c + 3] = v.w;
                 }
             }
@@ -2259,11 +2244,11 @@ __device__ __forceinline__ void seal_segment(const uint8_t *__restrict__ in0, u3
                     q0 = ldF(src); q1 = ldF(src + 16); q2 = ldF(src + 32);
                     q3 = ldP(src + 48, inlen - (64u * blk + 16u));
                 } else {
-                    const u32 o = 64u * blk - 32u;
-                    q0 = ldP(src, o < inlen ? inlen - o : 0u);
-                    q1 = ldP(src + 16, o + 16u < inlen ? inlen - o - 16u : 0u);
-                    q2 = ldP(src + 32, o + 32u < inlen ? inlen - o - 32u : 0u);
-                    q3 = ldP(src + 48, o + 48u < inlen ? inlen - o - 48u : 0u);
+                    const u64 o = 64u * blk - 32u;
+                    q0 = ldP(src, o < inlen ? inlen - o : 0);
+                    q1 = ldP(src + 16, o + 16 < inlen ? inlen - o - 16 : 0);
+                    q2 = ldP(src + 32, o + 32 < inlen ? inlen - o - 32 : 0);
+                    q3 = ldP(src + 48, o + 48 < inlen ? inlen - o - 48 : 0);
                 }
                 W[1] = q0.x; W[2] = q0.y; W[3] = q0.z; W[4] = q0.w;
                 W[5] = q1.x; W[6] = q1.y; W[7] = q1.z; W[8] = q1.w;
@@ -2275,24 +2260,17 @@ __device__ __forceinline__ void seal_segment(const uint8_t *__restrict__ in0, u3
             em.emit(q, C);
         }
     }
-    if (!has_rec) {
-        if constexpr (PARK) {
-            const uint4 pd = *reinterpret_cast<const uint4 *>(em.mine + 16);  // (this lane's own store)
-            P.p0 = pd.x; P.p1 = pd.y; P.p2 = pd.z; P.p3 = pd.w;
-        }
+    if (!rec) {
         u32 tag[4];
         poly_finish(P, tag);
         em.tag(tag);
     }
     em.close(false);  // convergent: a cooperative flush must see every lane of the wave
-    if (has_rec) {
-        u32 *rec = recp();
+    if (rec) {
         rec[0] = P.h0; rec[1] = P.h1; rec[2] = P.h2; rec[3] = P.h3; rec[4] = P.h4; rec[5] = mpoly;
         if (b0 == 0) {
             rec[8] = P.r0; rec[9] = P.r1; rec[10] = P.r2; rec[11] = P.r3;
-            if constexpr (!PARK) {
-                rec[12] = P.p0; rec[13] = P.p1; rec[14] = P.p2; rec[15] = P.p3;
-            }
+            rec[12] = P.p0; rec[13] = P.p1; rec[14] = P.p2; rec[15] = P.p3;
         }
     }
 }
@@ -2959,6 +2937,7 @@ __device__ __forceinline__ void seal_segments_body(const cz_frame_desc *__restri
     const bool live = t < nseg;
     const cz_segment sg = segs[live ? t : wave_first];
     const cz_frame_desc d = desc[sg.frame];
+    u32 *rec = sg.part == 0xffffffffu ? nullptr : work + 16ull * sg.part;
     const uint8_t *src = in + d.in_off;
     uint8_t *dst = out + d.out_off + 64ull * sg.first_block;
     const u32 b1 = sg.first_block + sg.nblocks;
@@ -2996,17 +2975,17 @@ __device__ __forceinline__ void seal_segments_body(const cz_frame_desc *__restri
                     EmitSegLinesSeal em{reinterpret_cast<uint4 *>(wl), dst, lane, total, 0u, 0u};
                     em.init(sg.first_block == 0);
                     seal_segment<true, EmitSegLinesSeal, true>(src, d.len, d.flags & 0xffu, d.counter, key,
-                                                           sg.first_block, b1, work, sg.part, em, wave_max(nch));
+                                                           sg.first_block, b1, rec, em, wave_max(nch));
                 } else {
                     EmitShiftLinesSeal em{wl, dst, lane, total, 0u, 0u};
                     em.init(sg.first_block == 0);
                     seal_segment<true, EmitShiftLinesSeal, true>(src, d.len, d.flags & 0xffu, d.counter, key,
-                                                             sg.first_block, b1, work, sg.part, em, wave_max(nch));
+                                                             sg.first_block, b1, rec, em, wave_max(nch));
                 }
             } else {
                 EmitSegLinesSeal em{reinterpret_cast<uint4 *>(wl), dst, lane, total, 0u, 0u};
                 em.init(sg.first_block == 0);
-                seal_segment<true>(src, d.len, d.flags & 0xffu, d.counter, key, sg.first_block, b1, work, sg.part, em);
+                seal_segment<true>(src, d.len, d.flags & 0xffu, d.counter, key, sg.first_block, b1, rec, em);
             }
             return;
         }
@@ -3021,10 +3000,10 @@ __device__ __forceinline__ void seal_segments_body(const cz_frame_desc *__restri
             em.init(sg.first_block == 0);
             if (__builtin_amdgcn_ballot_w64((((uintptr_t)src) & 7u) != 0u) == 0)
                 seal_segment<true, EmitShiftLinesSeal, true, 8>(src, d.len, d.flags & 0xffu, d.counter, key,
-                                                            sg.first_block, b1, work, sg.part, em, wave_max(nch));
+                                                            sg.first_block, b1, rec, em, wave_max(nch));
             else
                 seal_segment<true, EmitShiftLinesSeal, true, 1>(src, d.len, d.flags & 0xffu, d.counter, key,
-                                                            sg.first_block, b1, work, sg.part, em, wave_max(nch));
+                                                            sg.first_block, b1, rec, em, wave_max(nch));
             return;
         }
     }
@@ -3035,12 +3014,12 @@ __device__ __forceinline__ void seal_segments_body(const cz_frame_desc *__restri
             EmitDirect<true> em{dst, total};
             if (pair)
                 seal_segment<true, EmitDirect<true>, true>(src, d.len, d.flags & 0xffu, d.counter, key,
-                                                           sg.first_block, b1, work, sg.part, em);
+                                                           sg.first_block, b1, rec, em);
             else
-                seal_segment<true>(src, d.len, d.flags & 0xffu, d.counter, key, sg.first_block, b1, work, sg.part, em);
+                seal_segment<true>(src, d.len, d.flags & 0xffu, d.counter, key, sg.first_block, b1, rec, em);
         } else {
             EmitDirect<false> em{dst, total};
-            seal_segment<false>(src, d.len, d.flags & 0xffu, d.counter, key, sg.first_block, b1, work, sg.part, em);
+            seal_segment<false>(src, d.len, d.flags & 0xffu, d.counter, key, sg.first_block, b1, rec, em);
         }
     }
 }

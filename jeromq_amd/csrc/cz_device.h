@@ -188,41 +188,6 @@ __device__ __forceinline__ void salsa20_block_frame(u32 x[16], const SalsaFrame 
         x[i] = lazy_pending(i) ? ((x[i] ^ d[i]) + in[i]) : (x[i] + in[i]);
 }
 
-// Rounds 1-2 when the key and nonce word 6 are wave-uniform but the block counter c0 is not
-// (the segment kernels: each lane's segment starts at its own block).  Round 1's quarter-rounds
-// B, C, D come from the frame's words as above; of the rest only the first step of round 1's A
-// and three inputs of round 2 are uniform (~50 VALU against ~96 for per-lane rounds 1-2).
-__device__ __forceinline__ void rounds12_frame_lane(u32 x[16], const SalsaFrame &f, u32 c0, const u32 k[8])
-{
-#pragma unroll
-    for (int i = 0; i < 16; i++)
-        x[i] = f.w[i];
-    x[0] = SIGMA0; x[4] = k[3]; x[8] = c0; x[12] = k[5];
-    x[4] ^= srotl<7>(x[0] + x[12]);  x[8] ^= rotl(x[4] + x[0], 9);
-    x[12] ^= rotl(x[8] + x[4], 13);  x[0] ^= rotl(x[12] + x[8], 18);
-    // round 2 (rows); x4, x5, x6, x9, x10 are still uniform where srotl reads them
-    x[1] ^= rotl(x[0] + x[3], 7);    x[2] ^= rotl(x[1] + x[0], 9);
-    x[3] ^= rotl(x[2] + x[1], 13);   x[0] ^= rotl(x[3] + x[2], 18);
-    x[6] ^= srotl<7>(x[5] + x[4]);   x[7] ^= srotl<9>(x[6] + x[5]);
-    x[4] ^= rotl(x[7] + x[6], 13);   x[5] ^= rotl(x[4] + x[7], 18);
-    x[11] ^= srotl<7>(x[10] + x[9]); x[8] ^= rotl(x[11] + x[10], 9);
-    x[9] ^= rotl(x[8] + x[11], 13);  x[10] ^= rotl(x[9] + x[8], 18);
-    x[12] ^= rotl(x[15] + x[14], 7); x[13] ^= rotl(x[12] + x[15], 9);
-    x[14] ^= rotl(x[13] + x[12], 13); x[15] ^= rotl(x[14] + x[13], 18);
-}
-
-__device__ __forceinline__ void salsa20_block_frame_lane(u32 x[16], const SalsaFrame &f, const u32 k[8], u32 n0,
-                                                         u32 n1, u32 c0)
-{
-    const u32 in[16] = {SIGMA0, k[0], k[1], k[2], k[3], SIGMA1, n0, n1, c0, 0u, SIGMA2, k[4], k[5], k[6], k[7], SIGMA3};
-    u32 d[16];
-    rounds12_frame_lane(x, f, c0, k);
-    rounds_lazy<true>(x, d);
-#pragma unroll
-    for (int i = 0; i < 16; i++)
-        x[i] = lazy_pending(i) ? ((x[i] ^ d[i]) + in[i]) : (x[i] + in[i]);
-}
-
 // The last block of a box that uses at most 16 of its bytes (a 100-byte MESSAGE: 133-byte box, 5
 // bytes of block 2): keystream words 0..3 only.  Rounds 3..20 run the tail schedule
 // (cz_salsa_tail.h: the instructions words 0..3 depend on, 692 instead of 736) and the

@@ -2061,16 +2061,10 @@ __device__ __forceinline__ u32 seal_seg_bytes(u32 mlen, u32 b0, u32 bend)
 // most lines twice (2.6x the payload on the Zipf batch).
 // INA: as seal_frame's (16: 16-byte aligned payload; 8 / 1 with AL true: payload at an 8-byte /
 // any byte offset, read from the dword boundary at or above it with the funnel shift sh).
-// KS (key schedule): 0 -- per-lane key and nonce.  1 -- one key for the whole launch (in SGPRs)
-// and a wave-uniform high nonce word (the caller checks): keystream rounds 1-2 from the segment's
-// precomputed words (salsa_frame), per-lane block counters (rounds12_frame_lane).  2 -- as 1, and
-// every lane of the wave starts at the same block b0: scalar block counters (rounds12_frame).
-template <bool AL, class EM, bool PAIR = false, int INA = 16, int KS = 0>
+template <bool AL, class EM, bool PAIR = false, int INA = 16>
 __device__ __forceinline__ void seal_segment(const uint8_t *__restrict__ in0, u32 n, u32 flags, u64 counter, const u32 key[8], u32 b0,
                              u32 b1, u32 *__restrict__ rec, EM &em, u32 nrun = 0)
 {
-    if constexpr (KS == 2)
-        b0 = __builtin_amdgcn_readfirstlane(b0);
     static_assert(INA == 16 || AL, "INA 8/1 take the AL code paths");
     const u32 ina_a = INA == 1 ? (u32)(uintptr_t)in0 & 3u : 0u;
     const u32 ina_d = (4u - ina_a) & 3u;
@@ -2108,21 +2102,8 @@ __device__ __forceinline__ void seal_segment(const uint8_t *__restrict__ in0, u3
     const u64 inlen = n > ina_d ? (u64)(n - ina_d) : 0ull;
     u32 n0, n1;
     counter_nonce(counter, n0, n1);
-    if constexpr (KS != 0)
-        n0 = __builtin_amdgcn_readfirstlane(n0);
-    [[maybe_unused]] SalsaFrame sf{};
-    if constexpr (KS != 0)
-        sf = salsa_frame(key, n0, n1);
-    auto ksblock = [&](u32 *xs, u32 c0) {
-        if constexpr (KS == 2)
-            salsa20_block_frame(xs, sf, key, n0, n1, c0);
-        else if constexpr (KS == 1)
-            salsa20_block_frame_lane(xs, sf, key, n0, n1, c0);
-        else
-            salsa20_block(xs, key, n0, n1, c0, 0u);
-    };
     u32 x[16], C[16];
-    ksblock(x, 0u);
+    salsa20_block(x, key, n0, n1, 0u, 0u);
     Poly P;
     poly_init(P, x[0], x[1], x[2], x[3], x[4], x[5], x[6], x[7]);
     u32 mpoly = 0;
@@ -2131,7 +2112,7 @@ __device__ __forceinline__ void seal_segment(const uint8_t *__restrict__ in0, u3
     // own = false: a block past this lane's segment, run only to keep the wave in step
     // (PAIR with nrun > nch): not absorbed, and its stores are clipped by the emitter
     auto block = [&](u32 blk, const u32 *W, bool own = true) {
-        ksblock(x, blk);
+        salsa20_block(x, key, n0, n1, blk, 0u);
 #pragma unroll
         for (int k = 0; k < 16; k++)
             C[k] = funnel(W[k + 1], W[k], sh) ^ x[k];
@@ -2932,10 +2913,6 @@ __device__ __forceinline__ bool wave_lines_ok(bool full_wave, u32 nchunks, bool 
 constexpr int SEGMODE_REST = 4;   // k_seal_segments: only the waves k_seal_segments_lines leaves
 constexpr int SEGMODE_SHIFT16 = 8;  // 16-byte aligned outputs not all on 128-byte lines: EmitShiftLines
 constexpr int SEGMODE_ANYIN = 16;   // inputs at any byte offset on the line paths (dword-aligned loads)
-constexpr int SEGMODE_ONEKEY = 32;  // one key for every frame: `subkeys` is that key, key_idx is ignored
-#ifndef CZ_KU_B0
-#define CZ_KU_B0 1
-#endif
 
 // Segment kernels.  With line staging and whole-line loads enabled the launcher runs two
 // kernels over the same segment list: k_seal_segments_lines takes every full wave of aligned
@@ -2945,7 +2922,7 @@ constexpr int SEGMODE_ONEKEY = 32;  // one key for every frame: `subkeys` is tha
 // wave and unaligned buffers).  Without those modes k_seal_segments alone runs every wave.
 enum { SEGPART_ALL = 0, SEGPART_LINES = 1, SEGPART_REST = 2 };
 
-template <int PART, bool KU = false>
+template <int PART>
 __device__ __forceinline__ void seal_segments_body(const cz_frame_desc *__restrict__ desc,
                                                    const cz_segment *__restrict__ segs, uint32_t nseg,
                                                    const uint8_t *__restrict__ in, uint8_t *__restrict__ out,
@@ -2974,22 +2951,16 @@ __device__ __forceinline__ void seal_segments_body(const cz_frame_desc *__restri
     const bool in_al = (((uintptr_t)src) & 15u) == 0;
     const bool full_wave = wave_first + 64u <= nseg;
     const bool lines = allow_lines && (pair ? wave_lines_ragged_ok(full_wave, in_al) : wave_lines_ok(full_wave, nch, al));
-    // a one-key launch's line kernel needs one high nonce word per wave: a wave whose counters
-    // straddle 2^32 is left to the REST kernel
     if constexpr (PART == SEGPART_LINES) {
-        if (!lines || (KU && !wave_uniform((u32)(d.counter >> 32))))
+        if (!lines)
             return;
     }
     if constexpr (PART == SEGPART_REST) {
-        if (lines && (!(mode & SEGMODE_ONEKEY) || wave_uniform((u32)(d.counter >> 32))))
+        if (lines)
             return;
     }
-    static_assert(!KU || PART == SEGPART_LINES, "KU: the line-staged waves of a one-key launch");
     u32 key[8];
-    if (KU || (mode & SEGMODE_ONEKEY))
-        load_key(subkeys, key);  // KU: a uniform address, the key in SGPRs
-    else
-        load_key(subkeys + 32ull * d.key_idx, key);
+    load_key(subkeys + 32ull * d.key_idx, key);
     if constexpr (PART != SEGPART_REST) {
         if (lines) {
             const u32 lane = threadIdx.x & 63u;
@@ -3003,21 +2974,13 @@ __device__ __forceinline__ void seal_segments_body(const cz_frame_desc *__restri
                     (!(mode & SEGMODE_SHIFT16) || __builtin_amdgcn_ballot_w64(!line_al) == 0)) {
                     EmitSegLinesSeal em{reinterpret_cast<uint4 *>(wl), dst, lane, total, 0u, 0u};
                     em.init(sg.first_block == 0);
-                    if (KU && CZ_KU_B0 && wave_uniform(sg.first_block))
-                        seal_segment<true, EmitSegLinesSeal, true, 16, KU ? 2 : 0>(src, d.len, d.flags & 0xffu, d.counter, key,
-                                                                                sg.first_block, b1, rec, em, wave_max(nch));
-                    else
-                        seal_segment<true, EmitSegLinesSeal, true, 16, KU ? 1 : 0>(src, d.len, d.flags & 0xffu, d.counter, key,
-                                                                                sg.first_block, b1, rec, em, wave_max(nch));
+                    seal_segment<true, EmitSegLinesSeal, true>(src, d.len, d.flags & 0xffu, d.counter, key,
+                                                           sg.first_block, b1, rec, em, wave_max(nch));
                 } else {
                     EmitShiftLinesSeal em{wl, dst, lane, total, 0u, 0u};
                     em.init(sg.first_block == 0);
-                    if (KU && CZ_KU_B0 && wave_uniform(sg.first_block))
-                        seal_segment<true, EmitShiftLinesSeal, true, 16, KU ? 2 : 0>(src, d.len, d.flags & 0xffu, d.counter, key,
-                                                                                  sg.first_block, b1, rec, em, wave_max(nch));
-                    else
-                        seal_segment<true, EmitShiftLinesSeal, true, 16, KU ? 1 : 0>(src, d.len, d.flags & 0xffu, d.counter, key,
-                                                                                  sg.first_block, b1, rec, em, wave_max(nch));
+                    seal_segment<true, EmitShiftLinesSeal, true>(src, d.len, d.flags & 0xffu, d.counter, key,
+                                                             sg.first_block, b1, rec, em, wave_max(nch));
                 }
             } else {
                 EmitSegLinesSeal em{reinterpret_cast<uint4 *>(wl), dst, lane, total, 0u, 0u};
@@ -3082,16 +3045,6 @@ __global__ __launch_bounds__(BLOCK) CZ_SEG_LINES_OCC void k_seal_segments_lines(
 {
     extern __shared__ uint4 smem[];
     seal_segments_body<SEGPART_LINES>(desc, segs, nseg, in, out, subkeys, work, mode, smem);
-}
-
-// The same waves of a one-key launch (cz_seal_segments_key): `subkey` is the key of every frame
-__global__ __launch_bounds__(BLOCK) CZ_SEG_LINES_OCC void k_seal_segments_lines_key(
-    const cz_frame_desc *__restrict__ desc, const cz_segment *__restrict__ segs, uint32_t nseg,
-    const uint8_t *__restrict__ in, uint8_t *__restrict__ out, const uint8_t *__restrict__ subkey,
-    u32 *__restrict__ work, int mode)
-{
-    extern __shared__ uint4 smem[];
-    seal_segments_body<SEGPART_LINES, true>(desc, segs, nseg, in, out, subkey, work, mode, smem);
 }
 
 __global__ __launch_bounds__(BLOCK) void k_seal_combine(const cz_frame_desc *__restrict__ desc,
@@ -3944,15 +3897,9 @@ hipError_t czk_seal_segments(const cz_frame_desc *desc, const cz_segment *segs, 
 {
     const dim3 grid((nseg + BLOCK - 1) / BLOCK);
     if (nseg && g_seglines && g_pair) {
-#ifdef CZ_EXP_KU
-        const int mode = SEGMODE_LINES | SEGMODE_PAIR | (g_shift16 ? SEGMODE_SHIFT16 : 0) | (g_seal_ina ? SEGMODE_ANYIN : 0) | SEGMODE_ONEKEY;
-        hipLaunchKernelGGL(k_seal_segments_lines_key, grid, dim3(BLOCK), WAVES * SHIFT_LDS_BYTES, s, desc, segs, nseg,
-                           (const uint8_t *)in, (uint8_t *)out, (const uint8_t *)subkeys, (u32 *)work, mode);
-#else
         const int mode = SEGMODE_LINES | SEGMODE_PAIR | (g_shift16 ? SEGMODE_SHIFT16 : 0) | (g_seal_ina ? SEGMODE_ANYIN : 0);
         hipLaunchKernelGGL(k_seal_segments_lines, grid, dim3(BLOCK), WAVES * SHIFT_LDS_BYTES, s, desc, segs, nseg,
                            (const uint8_t *)in, (uint8_t *)out, (const uint8_t *)subkeys, (u32 *)work, mode);
-#endif
         hipLaunchKernelGGL(k_seal_segments, grid, dim3(BLOCK), g_seal_ina ? WAVES * SHIFT_LDS_BYTES : 0, s, desc, segs,
                            nseg, (const uint8_t *)in, (uint8_t *)out, (const uint8_t *)subkeys, (u32 *)work,
                            mode | SEGMODE_REST);

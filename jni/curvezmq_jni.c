@@ -54,6 +54,8 @@ typedef struct {
 
 static _Thread_local uint8_t *t_stage;
 static _Thread_local size_t t_stage_cap;
+/* staging kept between calls up to this size; a larger one (a big box) is freed after its call */
+#define STAGE_KEEP ((size_t)1 << 20)
 
 static size_t stage_round(jlong need) { return ((size_t)need + 15u) & ~(size_t)15u; }
 
@@ -104,6 +106,11 @@ static int stage_out(JNIEnv *env, jarr_arg *v, int n, size_t used, int rc)
                 (*env)->SetByteArrayRegion(env, v[i].a, 0, (jsize)v[i].need, (const jbyte *)v[i].p);
     if (used)
         explicit_bzero(t_stage, used);
+    if (t_stage_cap > STAGE_KEEP) {
+        free(t_stage);
+        t_stage = NULL;
+        t_stage_cap = 0;
+    }
     return rc;
 }
 

@@ -285,6 +285,14 @@ def test_jnacl_never_pins_across_the_library_call(shim):
     rc = getattr(L, JNACL + "crypto_1box_1keypair")(L.env, None, pk.obj, sk.obj)
     assert L.fake_lib_calls() == 1 and L.fake_lib_calls_pinned() == 0 and pk.pins() == sk.pins() == 0
     assert pk.sets() == sk.sets() == (1 if rc == 0 else 0)
+    # a box above the kept staging size (1 MiB): staged, freed after its call, then a small one again
+    for mlen in (3 << 20, 132):
+        big_c, big_m = Arr(L, np.zeros(mlen, np.uint8)), Arr(L, np.zeros(mlen, np.uint8))
+        _, _, n, k = _box_args(L)
+        L.fake_reset_lib_calls()
+        rc = getattr(L, JNACL + "crypto_1box_1afternm")(L.env, None, big_c.obj, big_m.obj, mlen, n.obj, k.obj)
+        assert L.fake_lib_calls() == 1 and L.fake_lib_calls_pinned() == 0 and big_m.gets() == 1
+        assert big_c.sets() == (1 if rc == 0 else 0)
     # the detector: a call made while some array is pinned is counted as such
     c, m, n, k = _box_args(L)
     other = Arr(L, np.zeros(8, np.uint8))
@@ -395,6 +403,18 @@ def test_jni_seal_open_through_the_shim(shim):
                 assert getattr(L, fn)(L.env, None, cc.obj, mm.obj, mlen, Arr(L, _u8(bytes.fromhex(v["nonce"]))).obj,
                                       Arr(L, _u8(bytes.fromhex(v["key"]))).obj) == 0, (fn, mlen)
                 assert cc.np.tobytes().hex() == v["c"], (fn, mlen)
+        # a 3 MiB box (past the 1 MiB of staging kept between calls) round-trips, and the 133-byte box
+        # after it seals to the same bytes as before
+        big = np.zeros(3 << 20, dtype=np.uint8)
+        big[32:] = _u8(splitmix_bytes(big.size - 32, 12))
+        bc, bm = Arr(L, np.zeros(big.size, np.uint8)), Arr(L, big)
+        assert getattr(L, JNACL + "crypto_1box_1afternm")(L.env, None, bc.obj, bm.obj, big.size, n.obj, k.obj) == 0
+        bb = Arr(L, np.zeros(big.size, np.uint8))
+        assert getattr(L, JNACL + "crypto_1box_1open_1afternm")(L.env, None, bb.obj, bc.obj, big.size, n.obj, k.obj) == 0
+        assert np.array_equal(bb.np, big)
+        c2 = Arr(L, np.zeros(133, np.uint8))
+        assert getattr(L, JNACL + "crypto_1box_1afternm")(L.env, None, c2.obj, ma.obj, 133, n.obj, k.obj) == 0
+        assert c2.np[16:].tobytes() == body[16:]
         assert L.fake_outstanding() == 0 and L.fake_calls_in_critical() == 0 and L.fake_lib_calls_pinned() == 0
     finally:
         L.fake_set_copy_mode(0)

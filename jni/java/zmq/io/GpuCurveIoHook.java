@@ -208,6 +208,9 @@ public final class GpuCurveIoHook implements AutoCloseable
                 c.held = msg;      // the arena is full: this one leads the next loop
                 return true;
             }
+            if (c.failed) {
+                return false;      // queue() tore the connection down: pull nothing more
+            }
             msg = c.sink.pull();
         }
         return c.queued;
@@ -217,14 +220,16 @@ public final class GpuCurveIoHook implements AutoCloseable
     {
         final int size = msg.size();
         final int flags = (msg.hasMore() ? Msg.MORE : 0) | (msg.isCommand() ? Msg.COMMAND : 0);
-        ByteBuffer payload = msg.buf();   // position 0: Msg never moves its buffer's position
+        // Msg.buf() is a duplicate at the Msg's own position (not always 0, Msg.java:146-155): slice it,
+        // so that the direct address the engine takes is the payload's first byte
+        ByteBuffer payload = msg.buf().slice();
+        payload.limit(size);
         if (!payload.isDirect()) {
             // a heap payload (not from pinnedMsg()): one copy into the arena
             ByteBuffer pinned = GpuCurveEngine.msgAlloc(engine, size);
             if (pinned == null) {
                 return false;
             }
-            payload.limit(size);
             pinned.put(payload);
             pinned.flip();
             payload = pinned;

@@ -164,7 +164,7 @@ final class GpuCurveMessageBatch implements AutoCloseable
             Msg m = msgs.get(i);
             io = up16(io);
             oo = up16(oo);
-            ByteBuffer src = m.buf();            // position 0 (Msg never moves it)
+            ByteBuffer src = m.buf().slice();    // from the Msg's own position (Msg.java:146-155)
             src.limit(m.size());
             ByteBuffer dst = in.duplicate();
             dst.position((int) io);
@@ -214,7 +214,7 @@ final class GpuCurveMessageBatch implements AutoCloseable
             Msg m = bodies.get(i);
             io = up16(io);
             oo = up16(oo);
-            ByteBuffer src = m.buf();
+            ByteBuffer src = m.buf().slice();
             src.limit(m.size());
             ByteBuffer dst = in.duplicate();
             dst.position((int) io);

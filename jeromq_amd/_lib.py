@@ -179,6 +179,18 @@ SIGNATURES = {
 _LIB = None
 
 
+def _torch_runtime_first():
+    """PyTorch bundles its own libamdhip64 / libhsa-runtime64, loaded into the global symbol scope by
+    `import torch`.  Importing torch before the library binds the library's HIP calls to that same
+    runtime: one runtime in the process.  Loaded the other way round, the process holds two, and
+    whichever initializes second sees no device (tools/diag/hip_init_order.py,
+    profiles/r06/hip_init_order.log).  torch is imported only, not initialized."""
+    try:
+        import torch  # noqa: F401
+    except ImportError:
+        pass
+
+
 def lib():
     """Load the HIP library; raise loudly if it has not been built."""
     global _LIB
@@ -187,6 +199,7 @@ def lib():
     if not os.path.exists(LIB_PATH):
         raise CzError(f"{LIB_PATH} is missing: run `python -m jeromq_amd.build` (hipcc, gfx950). "
                       "There is no CPU fallback for the CURVE path.")
+    _torch_runtime_first()
     L = ctypes.CDLL(LIB_PATH)
     ab_variant = "CZ_LIB" in os.environ  # an older A/B build may predate a symbol; the product may not
     for name, (res, args) in SIGNATURES.items():

@@ -56,6 +56,8 @@ def shim(tmp_path_factory):
                     "-I" + JNI, "-I" + os.path.join(ROOT, "include"), os.path.join(JNI, "curvezmq_jni.c"),
                     os.path.join(JNI, "fake_jni_env.c"), "-L" + LIBDIR, "-lcurvezmq_mi355x",
                     "-Wl,-rpath," + LIBDIR, "-Wl," + wraps, "-o", out], check=True)
+    from jeromq_amd import _lib
+    _lib._torch_runtime_first()   # the shim's library on torch's HIP runtime, as _lib.lib() loads it
     L = ctypes.CDLL(out)
     for f in ("fake_env", "fake_byte_array", "fake_int_array", "fake_direct", "fake_heap_buffer", "fake_elem",
               "fake_addr"):
@@ -357,9 +359,14 @@ def test_uniform_strides_that_overflow_are_refused(shim):
 
 
 def _has_gpu():
+    """device_count() does not initialize torch's HIP runtime.  is_available() would, and torch
+    bundles its own libamdhip64: a process that has loaded the library (here through the shim) and
+    then initializes torch's runtime before the library's first HIP call leaves the library with no
+    device (tools/diag/hip_init_order.py: lib-torch-call fails; lib-call, lib-count-call and
+    torch-lib-call work)."""
     try:
         import torch
-        return torch.cuda.is_available()
+        return torch.cuda.device_count() > 0
     except Exception:
         return False
 
@@ -381,7 +388,9 @@ def test_jni_seal_open_through_the_shim(shim):
         c, n, k = (Arr(L, np.zeros(133, np.uint8)), Arr(L, _u8(b"CurveZMQMESSAGEC" + (3).to_bytes(8, "big"))),
                    Arr(L, _u8(PRECOM)))
         ma = Arr(L, m)
-        assert getattr(L, JNACL + "crypto_1box_1afternm")(L.env, None, c.obj, ma.obj, 133, n.obj, k.obj) == 0
+        from jeromq_amd import _lib
+        rc = getattr(L, JNACL + "crypto_1box_1afternm")(L.env, None, c.obj, ma.obj, 133, n.obj, k.obj)
+        assert rc == 0, _lib.last_error()
         body = or_curve_encode(payload, 1, 3, 0, PRECOM)     # "\x07MESSAGE" || nonce[16:24] || box[16:]
         assert c.np[:16].tobytes() == bytes(16) and c.np[16:].tobytes() == body[16:]
         back = Arr(L, np.full(133, 0xAA, np.uint8))

@@ -2610,7 +2610,7 @@ __device__ __forceinline__ void seal_uniform_body(const uint8_t *__restrict__ in
 
 #ifdef CZ_DIAG_CLOCK
 // Clock diagnostic (tools/build_variant.sh NAME -DCZ_DIAG_CLOCK, tools/clock_stamp.py): every wave of
-// k_seal_uniform stamps the shader clock counter (s_memtime) and the 100 MHz constant counter
+// k_seal_uniform and k_open_uniform stamps the shader clock counter (s_memtime) and the 100 MHz constant counter
 // (s_memrealtime) when it starts and when it leaves; lane 0 writes the four values with a vector
 // store.  Wave clock = d(memtime) / d(realtime) * 100 MHz, unprofiled.  Output bytes are unchanged.
 constexpr u32 DIAG_CLOCK_WAVES = 1u << 16;
@@ -2726,6 +2726,15 @@ __global__ __launch_bounds__(BLOCK) void k_open_desc(const cz_frame_desc *__rest
 // INA (open_frame): 16 for 16-byte aligned bodies; 8 / 1 for bodies at 8-byte / any byte offsets
 // (the dense wire layout), line-staged (ST_LINES) plaintext only
 // (at least 3 waves per SIMD: the byte-shifted plaintext staging needs 170-179 VGPRs uncapped)
+#ifdef CZ_DIAG_CLOCK
+// the clock build stamps every wave around the body (k_open_uniform below); the product kernel is
+// the body itself, so its machine code does not change with the diagnostic
+template <int ST, bool PAIR, int INA>
+__device__ __forceinline__ void open_uniform_body(const uint8_t *__restrict__ in, uint64_t in_stride,
+                                                  uint8_t *__restrict__ out, uint64_t out_stride, uint32_t count,
+                                                  uint32_t size, const uint8_t *__restrict__ subkey, uint64_t floor0,
+                                                  int check, uint16_t *__restrict__ status, int allow_un0, int prev0)
+#else
 template <int ST, bool PAIR, int INA = 16>
 __global__ __launch_bounds__(BLOCK) CZ_OCC CZ_OPEN_UNI_OCC void k_open_uniform(const uint8_t *__restrict__ in, uint64_t in_stride,
                                                          uint8_t *__restrict__ out, uint64_t out_stride,
@@ -2733,6 +2742,7 @@ __global__ __launch_bounds__(BLOCK) CZ_OCC CZ_OPEN_UNI_OCC void k_open_uniform(c
                                                          const uint8_t *__restrict__ subkey, uint64_t floor0,
                                                          int check, uint16_t *__restrict__ status, int allow_un0,
                                                          int prev0 = 0)
+#endif
 {
     // prev0: frame 0's floor is the nonce of the body in_stride bytes before it (a tail launched
     // behind the phase-sorted carry kernel), not floor0
@@ -2828,6 +2838,22 @@ __global__ __launch_bounds__(BLOCK) CZ_OCC CZ_OPEN_UNI_OCC void k_open_uniform(c
             zero_bytes(dst + nout, (u32)(out_stride - nout));
     status[i] = (uint16_t)(st | (st == CZ_STATUS_OK ? (fl << 8) : 0u));
 }
+
+#ifdef CZ_DIAG_CLOCK
+template <int ST, bool PAIR, int INA = 16>
+__global__ __launch_bounds__(BLOCK) CZ_OCC CZ_OPEN_UNI_OCC void k_open_uniform(const uint8_t *__restrict__ in, uint64_t in_stride,
+                                                         uint8_t *__restrict__ out, uint64_t out_stride,
+                                                         uint32_t count, uint32_t size,
+                                                         const uint8_t *__restrict__ subkey, uint64_t floor0,
+                                                         int check, uint16_t *__restrict__ status, int allow_un0,
+                                                         int prev0 = 0)
+{
+    CZ_DIAG_CLOCK_BEGIN
+    open_uniform_body<ST, PAIR, INA>(in, in_stride, out, out_stride, count, size, subkey, floor0, check, status,
+                                     allow_un0, prev0);
+    CZ_DIAG_CLOCK_END
+}
+#endif
 
 // Phase-sorted open of bodies off 16-byte alignment into line-aligned plaintext slots (the dense
 // wire layout: V2Decoder leaves bodies back to back, zmq/io/coder/v2/V2Decoder.java:67-105).
@@ -3851,6 +3877,18 @@ hipError_t czk_open_uniform(const void *in, uint64_t in_stride, void *out, uint6
 #undef CZ_OPEN_LAUNCH_INA
     return hipGetLastError();
 }
+
+#ifdef CZ_DIAG_CLOCK
+// diagnostic builds only: the last k_open_uniform launch's wave stamps (this part's g_diag_clock)
+extern "C" __attribute__((visibility("default"))) int cz_diag_clock_read_open(uint64_t *host, uint64_t waves)
+{
+    if (waves > DIAG_CLOCK_WAVES)
+        waves = DIAG_CLOCK_WAVES;
+    return hipMemcpyFromSymbol(host, HIP_SYMBOL(g_diag_clock), waves * 32u, 0, hipMemcpyDeviceToHost) == hipSuccess
+               ? (int)waves
+               : -1;
+}
+#endif
 
 #endif  // CZ_KPART_HAS(2)
 

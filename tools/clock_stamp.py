@@ -2,6 +2,7 @@
 
   bash tools/build_variant.sh clock -DCZ_DIAG_CLOCK
   CZ_LIB=$PWD/jeromq_amd/libcz_clock.so python tools/clock_stamp.py [--ramp-s 3] [--launches 20]
+      [--config 4k|4k_dense|4k_box|100b|open4k] [--plain-stride 4224]
 
 The diagnostic build stamps s_memtime (shader clock counter) and s_memrealtime (constant 100 MHz
 counter) per wave of k_seal_uniform when the wave starts and when it leaves (cz_kernels.hip,
@@ -37,17 +38,21 @@ def main():
     ap.add_argument("--ramp-s", type=float, default=3.0)
     ap.add_argument("--launches", type=int, default=20)
     ap.add_argument("--frames", type=int, default=1 << 20)
+    ap.add_argument("--config", default="4k", choices=["4k", "4k_dense", "4k_box", "100b", "open4k"],
+                    help="a bench config on k_seal_uniform, or open4k on k_open_uniform")
+    ap.add_argument("--plain-stride", type=int, default=0, help="open4k: plaintext slot stride")
     a = ap.parse_args()
     if "CZ_LIB" not in os.environ:
         raise SystemExit("set CZ_LIB to a -DCZ_DIAG_CLOCK build (tools/build_variant.sh clock -DCZ_DIAG_CLOCK)")
     L = _lib.lib()
     if not hasattr(L, "cz_diag_clock_read"):
         raise SystemExit(f"{_lib.LIB_PATH} has no cz_diag_clock_read: not a -DCZ_DIAG_CLOCK build")
-    L.cz_diag_clock_read.restype = ctypes.c_int
-    L.cz_diag_clock_read.argtypes = [ctypes.c_void_p, ctypes.c_uint64]
+    read = L.cz_diag_clock_read_open if a.config == "open4k" else L.cz_diag_clock_read
+    read.restype = ctypes.c_int
+    read.argtypes = [ctypes.c_void_p, ctypes.c_uint64]
     dev = torch.device("cuda:0")
     torch.cuda.set_device(0)
-    wl = bench.Workload("4k", a.frames, 0, dev)
+    wl = bench.Workload(a.config, a.frames, 0, dev, plain_stride=a.plain_stride)
     waves = (a.frames + 63) // 64
     s = torch.cuda.current_stream()
     t0 = time.perf_counter()
@@ -67,7 +72,7 @@ def main():
         wl.step()
         eb.record(s)
         torch.cuda.synchronize()
-        n = L.cz_diag_clock_read(buf.ctypes.data, waves)
+        n = read(buf.ctypes.data, waves)
         assert n == waves, n
         st = buf.reshape(waves, 4).astype(np.float64)
         dt, dr = st[:, 2] - st[:, 0], st[:, 3] - st[:, 1]
@@ -82,11 +87,13 @@ def main():
                      "resident_waves_mean": float(dr[ok].sum() / span_rt)})
         for _ in range(4):   # queued ahead of the next measured launch: it starts with no idle gap
             wl.step()
-    pmc = bench.load_pmc("4k")
+    pmc = bench.load_pmc(a.config)
     valu = pmc.get("valu_insts_per_launch")
     clk = statistics.median(r["clock_ghz_median"] for r in rows)
     kms = statistics.median(r["kernel_ms"] for r in rows)
-    res = {"what": "k_seal_uniform (headline 2^20 x 4 KiB seal), per-wave s_memtime / s_memrealtime stamps, unprofiled",
+    kern = "k_open_uniform" if a.config == "open4k" else "k_seal_uniform"
+    res = {"what": f"{kern} (bench config {a.config}" + (f", {a.plain_stride}-byte plaintext slots" if a.plain_stride else "")
+           + f", {a.frames} frames), per-wave s_memtime / s_memrealtime stamps, unprofiled",
            "lib": os.path.basename(_lib.LIB_PATH), "ramp_launches": ramp, "ramp_s": round(ramp_s, 2),
            "launches": len(rows), "kernel_ms_median": round(kms, 4),
            "clock_ghz_median": round(clk, 4),

@@ -56,7 +56,7 @@ for key in 4k zipf open4k 100b 4k_dense 4k_box zipf@ia8,oa8 zipf@oa1 zipf_open@i
 done
 fi
 if has pmc; then
-bash tools/gpu_traffic.sh 4k 100b zipf open4k 4k_dense 4k_box zipf@oa1 zipf_open@ia8,oa8 open4k@os4129 open4k@os4136 || exit 7
+bash tools/gpu_traffic.sh 4k 100b zipf open4k 4k_dense 4k_box zipf@ia8,oa8 zipf@oa1 zipf_open@ia8,oa8 open4k@os4129 open4k@os4136 || exit 7
 bash tools/gpu_valu.sh 4k 100b zipf open4k 4k_dense 4k_box zipf@ia8,oa8 zipf@oa1 zipf_open@ia8,oa8 open4k@os4129 open4k@os4136 || exit 8
 bash tools/gpu_stall.sh 4k open4k zipf > gpurun_out/stall_measure.log 2>&1 || { tail gpurun_out/stall_measure.log; exit 9; }
 cp profiles/pmc_traffic.json gpurun_out/pmc_traffic_measure.json

@@ -55,3 +55,15 @@ def test_no_rejected_variant_switches_in_product_sources():
             text = open(os.path.join(csrc, f)).read()
             assert not [g for g in gone if g in text], f
             assert "CZ_DIAG_NOSTORE_ALL" not in text or f == "cz_diag.h", f
+
+
+def test_loader_imports_torch_before_the_library():
+    """One HIP runtime per process: jeromq_amd._lib.lib() imports torch, whose
+    bundled libamdhip64 then serves the library's HIP calls, before it dlopens the library."""
+    import inspect
+    import sys
+    from jeromq_amd import _lib
+    src = inspect.getsource(_lib.lib)
+    assert src.index("_torch_runtime_first()") < src.index("ctypes.CDLL(LIB_PATH)")
+    _lib._torch_runtime_first()
+    assert "torch" in sys.modules

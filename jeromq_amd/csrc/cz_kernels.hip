@@ -2610,7 +2610,7 @@ __device__ __forceinline__ void seal_uniform_body(const uint8_t *__restrict__ in
 
 #ifdef CZ_DIAG_CLOCK
 // Clock diagnostic (tools/build_variant.sh NAME -DCZ_DIAG_CLOCK, tools/clock_stamp.py): every wave of
-// k_seal_uniform and k_open_uniform stamps the shader clock counter (s_memtime) and the 100 MHz constant counter
+// k_seal_uniform, k_open_uniform and k_seal_segments_lines stamps the shader clock counter (s_memtime) and the 100 MHz constant counter
 // (s_memrealtime) when it starts and when it leaves; lane 0 writes the four values with a vector
 // store.  Wave clock = d(memtime) / d(realtime) * 100 MHz, unprofiled.  Output bytes are unchanged.
 constexpr u32 DIAG_CLOCK_WAVES = 1u << 16;
@@ -3070,7 +3070,9 @@ __global__ __launch_bounds__(BLOCK) CZ_SEG_LINES_OCC void k_seal_segments_lines(
     u32 *__restrict__ work, int mode)
 {
     extern __shared__ uint4 smem[];
+    CZ_DIAG_CLOCK_BEGIN
     seal_segments_body<SEGPART_LINES>(desc, segs, nseg, in, out, subkeys, work, mode, smem);
+    CZ_DIAG_CLOCK_END
 }
 
 __global__ __launch_bounds__(BLOCK) void k_seal_combine(const cz_frame_desc *__restrict__ desc,
@@ -4046,6 +4048,18 @@ hipError_t czk_fill(void *buf, uint64_t nbytes, uint64_t seed, hipStream_t s)
     hipLaunchKernelGGL(k_fill, grid, dim3(BLOCK), 0, s, (uint8_t *)buf, nbytes, seed);
     return hipGetLastError();
 }
+
+#ifdef CZ_DIAG_CLOCK
+// diagnostic builds only: the last k_seal_segments_lines launch's wave stamps (this part's g_diag_clock)
+extern "C" __attribute__((visibility("default"))) int cz_diag_clock_read_seg(uint64_t *host, uint64_t waves)
+{
+    if (waves > DIAG_CLOCK_WAVES)
+        waves = DIAG_CLOCK_WAVES;
+    return hipMemcpyFromSymbol(host, HIP_SYMBOL(g_diag_clock), waves * 32u, 0, hipMemcpyDeviceToHost) == hipSuccess
+               ? (int)waves
+               : -1;
+}
+#endif
 
 #endif  // CZ_KPART_HAS(3)
 

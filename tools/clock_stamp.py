@@ -38,8 +38,8 @@ def main():
     ap.add_argument("--ramp-s", type=float, default=3.0)
     ap.add_argument("--launches", type=int, default=20)
     ap.add_argument("--frames", type=int, default=1 << 20)
-    ap.add_argument("--config", default="4k", choices=["4k", "4k_dense", "4k_box", "100b", "open4k"],
-                    help="a bench config on k_seal_uniform, or open4k on k_open_uniform")
+    ap.add_argument("--config", default="4k", choices=["4k", "4k_dense", "4k_box", "100b", "open4k", "zipf"],
+                    help="a bench config on k_seal_uniform, open4k on k_open_uniform, zipf on k_seal_segments_lines")
     ap.add_argument("--plain-stride", type=int, default=0, help="open4k: plaintext slot stride")
     a = ap.parse_args()
     if "CZ_LIB" not in os.environ:
@@ -47,13 +47,15 @@ def main():
     L = _lib.lib()
     if not hasattr(L, "cz_diag_clock_read"):
         raise SystemExit(f"{_lib.LIB_PATH} has no cz_diag_clock_read: not a -DCZ_DIAG_CLOCK build")
-    read = L.cz_diag_clock_read_open if a.config == "open4k" else L.cz_diag_clock_read
+    read = {"open4k": L.cz_diag_clock_read_open, "zipf": L.cz_diag_clock_read_seg}.get(a.config, L.cz_diag_clock_read)
     read.restype = ctypes.c_int
     read.argtypes = [ctypes.c_void_p, ctypes.c_uint64]
     dev = torch.device("cuda:0")
     torch.cuda.set_device(0)
     wl = bench.Workload(a.config, a.frames, 0, dev, plain_stride=a.plain_stride)
-    waves = (a.frames + 63) // 64
+    # zipf: the lines kernel's waves over the segment list (the waves it leaves to the REST kernel
+    # stamp a few cycles each and weigh nothing in the duration-weighted clock)
+    waves = (wl.plan.nseg + 63) // 64 if a.config == "zipf" else (a.frames + 63) // 64
     s = torch.cuda.current_stream()
     t0 = time.perf_counter()
     ramp = 0
@@ -81,6 +83,7 @@ def main():
         kern_s = ea.elapsed_time(eb) / 1e3
         span_rt = (st[:, 3].max() - st[:, 1].min())
         rows.append({"kernel_ms": kern_s * 1e3, "clock_ghz_median": float(np.median(clk)),
+                     "clock_ghz_weighted": float(dt[ok].sum() / dr[ok].sum() * RT_HZ / 1e9),
                      "clock_ghz_p10": float(np.percentile(clk, 10)), "clock_ghz_p90": float(np.percentile(clk, 90)),
                      "realtime_hz_check": span_rt / kern_s,
                      "wave_us_median": float(np.median(dr[ok])) / RT_HZ * 1e6,
@@ -89,14 +92,20 @@ def main():
             wl.step()
     pmc = bench.load_pmc(a.config)
     valu = pmc.get("valu_insts_per_launch")
-    clk = statistics.median(r["clock_ghz_median"] for r in rows)
+    # per-wave median for the uniform kernels (every wave alike); duration-weighted for the segment
+    # kernel, whose early-exit waves would otherwise count as much as a 128-block segment
+    clk_key = "clock_ghz_weighted" if a.config == "zipf" else "clock_ghz_median"
+    clk = statistics.median(r[clk_key] for r in rows)
     kms = statistics.median(r["kernel_ms"] for r in rows)
-    kern = "k_open_uniform" if a.config == "open4k" else "k_seal_uniform"
+    kern = {"open4k": "k_open_uniform", "zipf": "k_seal_segments_lines (+ REST and combine launches in the timed step)"}.get(
+        a.config, "k_seal_uniform")
     res = {"what": f"{kern} (bench config {a.config}" + (f", {a.plain_stride}-byte plaintext slots" if a.plain_stride else "")
            + f", {a.frames} frames), per-wave s_memtime / s_memrealtime stamps, unprofiled",
            "lib": os.path.basename(_lib.LIB_PATH), "ramp_launches": ramp, "ramp_s": round(ramp_s, 2),
            "launches": len(rows), "kernel_ms_median": round(kms, 4),
-           "clock_ghz_median": round(clk, 4),
+           "clock_ghz_median": round(statistics.median(r["clock_ghz_median"] for r in rows), 4),
+           "clock_ghz_weighted": round(statistics.median(r["clock_ghz_weighted"] for r in rows), 4),
+           "clock_used": clk_key,
            "clock_ghz_p10_median": round(statistics.median(r["clock_ghz_p10"] for r in rows), 4),
            "clock_ghz_p90_median": round(statistics.median(r["clock_ghz_p90"] for r in rows), 4),
            "realtime_hz_check_median": round(statistics.median(r["realtime_hz_check"] for r in rows), 0),
